@@ -1,0 +1,73 @@
+/*
+ * snake_oracle.h -- CPU restatement of the reference SnakeEnv (TEST INFRASTRUCTURE).
+ *
+ * This is the parity ORACLE, not the product. Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it, and only as the checker / the
+ * timed CPU baseline. The product path (marl-snake_amd/csrc, include/snake_env.h)
+ * never links or calls it.
+ *
+ * Restates, serially and literally, tranthai189765/MARL-Snake:
+ *   marlenv/marlenv/envs/snake_env.py  (SnakeEnv.__init__/reset/step/_encode/...)
+ *   marlenv/marlenv/core/snake.py      (Cell, Direction, Snake)
+ *   marlenv/marlenv/core/grid_util.py  (make_grid, dfs_sweep_empty, random_empty_coords, draw)
+ *   numpy legacy RandomState (MT19937 init_genrand, random_interval, masked randint),
+ *   pinned numpy==1.21.0 (marlenv/requirements.txt:2); the legacy stream is frozen.
+ * Pinned against the tests/golden fixtures (generated from the real reference by
+ * tests/golden/gen/make_golden.py).
+ */
+#ifndef SNAKE_ORACLE_H
+#define SNAKE_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct so_env so_env;
+
+typedef struct {
+    int32_t height, width, num_snakes, snake_length;
+    int32_t vision_range;     /* 0 == None (full map) */
+    int32_t frame_stack;
+    int32_t observer;         /* 0 = 'snake' (3 relative actions), 1 = 'human' (5 absolute) */
+    int32_t num_fruits;
+    double  rew_fruit, rew_kill, rew_lose, rew_win, rew_time;
+    double  max_episode_steps;
+} so_cfg;
+
+typedef struct {
+    int64_t rank[16];
+    double  scores[16], steps[16], fruits[16], kills[16];
+} so_info;
+
+/* ---- env ---------------------------------------------------------------- */
+so_env *so_create(const so_cfg *cfg, uint32_t seed);   /* np.random.seed(seed) + SnakeEnv(**cfg) */
+void    so_destroy(so_env *e);
+int64_t so_obs_size(const so_env *e);                  /* S*h*w*8*fs bytes */
+int     so_reset(so_env *e, uint8_t *obs);             /* snake_env.py:131-159 */
+/* snake_env.py:301-414. Returns 1 when all dones (info filled), 0 otherwise,
+ * -1 on an invalid action for an alive snake (the reference's KeyError). */
+int     so_step(so_env *e, const int32_t *actions, uint8_t *obs, double *rews,
+                uint8_t *dones, so_info *info);
+void    so_get_grid(const so_env *e, int8_t *out);     /* H*W */
+int64_t so_alive_snakes(const so_env *e);
+int64_t so_episode_length(const so_env *e);
+/* per snake: head r,c, tail r,c, dir (0 UP,1 RIGHT,2 DOWN,3 LEFT), alive, length(cells) */
+void    so_get_snakes(const so_env *e, int32_t *out7xS);
+/* Inject a crafted state exactly as tests/golden/gen/make_golden.py:inject does:
+ * grid (H*W, int32), snake k = coords[off[k]..off[k+1]) as (r,c) pairs, alive flags. */
+int     so_inject(so_env *e, const int32_t *grid, const int32_t *coords, const int32_t *off,
+                  const uint8_t *alive, int64_t alive_snakes, int64_t episode_length);
+
+/* ---- RNG / tables (checked against tests/golden/rng.npz, candidates.npz) -- */
+void    so_rng_raw(uint32_t seed, int64_t n, uint32_t *out);
+/* randint(0, n, size=k) after seed(seed); *next = the following raw draw */
+void    so_rng_randint(uint32_t seed, int64_t n, int64_t k, int64_t *out, uint32_t *next);
+void    so_rng_permutation(uint32_t seed, int64_t n, int64_t *out, uint32_t *next);
+/* dfs_sweep_empty(make_grid(H,W), L): writes C*L*2 int16 (r,c) if out != NULL; returns C */
+int64_t so_candidates(int32_t H, int32_t W, int32_t L, int16_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
