@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Throughput of the batched multi-snake env step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Workload (BASELINE.json metric, config 3): 65 536 envs per GPU of 20x20 grids,
+4 snakes, vision_range=5, frame_stack=1, snake_length=3, default rewards,
+uniform random actions in {0,1,2} drawn up front on the device (seed 12345),
+all-done auto-reset inside the step. Env i is seeded with its GLOBAL index, so
+ranks hold disjoint shards of one big batch (weak scaling, no collective on the
+step path; the only collectives are the timing barrier and max-reduce).
+
+A step = one SnakeVecEnv.step() over the GPU's whole batch. The timed region is
+exactly K steps between barrier + synchronize on both sides; value = all envs of
+all ranks x K / the slowest rank's time.
+
+The JSON line also carries:
+  roofline     -- the step kernel's algorithmic HBM bytes (SURVEY.md 8(d):
+                  B = S*h*w*8*fs + (fs+1)*H*W + 10*S per env-step) / its average
+                  duration, timed with HIP events on the launch stream during the
+                  timed region, against the 8 TB/s HBM peak; `traffic` = HBM bytes
+                  per launch from rocprofv3 PMC counters when profiles/pmc_traffic.json
+                  holds a measurement for this workload, else null.
+  cpu_baseline -- rank 0 at N=1: the CPU restatement (oracle/, a C port of the
+                  reference SnakeEnv, 1 core) timed on a bounded sample of the same
+                  workload on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, 'marl-snake_amd'), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = 'env-steps/sec whole-node, 65536×(20×20, 4 snakes), random actions; 1→8 GPU'
+HBM_PEAK_GBS = 8000.0
+
+
+def shard_range(n_total, world, rank):
+    """Contiguous env range [lo, hi) of one rank."""
+    base, extra = divmod(n_total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def algorithmic_bytes(S, h, w, fs, H, W):
+    """obs write + grid ring read/write + actions/rewards/dones."""
+    return S * h * w * 8 * fs + (fs + 1) * H * W + S * (1 + 8 + 1)
+
+
+def cpu_baseline(env_kw, num_snakes, seconds):
+    """CPU restatement of the reference step (oracle/, C, one core) on a bounded sample."""
+    import numpy as np
+    from oracle.snake_oracle import OracleEnv
+    n_env = 16
+    envs = [OracleEnv(seed=i, num_snakes=num_snakes, **env_kw) for i in range(n_env)]
+    for e in envs:
+        e.reset()
+    rs = np.random.RandomState(12345)
+    acts = rs.randint(0, 3, size=(4096, n_env, num_snakes))
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        a = acts[(steps // n_env) % 4096]
+        for i, e in enumerate(envs):
+            _, _, d, _ = e.step(a[i])
+            if d.all():
+                e.reset()
+        steps += n_env
+    el = time.perf_counter() - t0
+    return dict(value=round(steps / el, 1), unit='env-steps/s', cores=1, kind='port',
+                sample=f'{n_env} envs x {steps // n_env} steps incl. auto-resets, {el:.1f} s, '
+                       f'oracle/snake_oracle.c (serial C restatement of SnakeEnv.step/reset)')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=500)
+    ap.add_argument('--warmup', type=int, default=200)
+    ap.add_argument('--envs-per-gpu', type=int, default=65536)
+    ap.add_argument('--height', type=int, default=20)
+    ap.add_argument('--width', type=int, default=20)
+    ap.add_argument('--num-snakes', type=int, default=4)
+    ap.add_argument('--vision-range', type=int, default=5)
+    ap.add_argument('--frame-stack', type=int, default=1)
+    ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit('--gpus N>1 needs one process per GPU: launch with torch.distributed.run')
+    distributed = world > 1
+    if distributed:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    device = torch.device('cuda', local_rank if distributed else torch.cuda.current_device())
+
+    from marlenv import SnakeVecEnv
+
+    per = args.envs_per_gpu
+    n_total = per * world
+    lo, hi = shard_range(n_total, world, rank)
+    env_kw = dict(height=args.height, width=args.width, snake_length=3,
+                  vision_range=args.vision_range or None, frame_stack=args.frame_stack)
+    S = args.num_snakes
+    venv = SnakeVecEnv(hi - lo, num_snakes=S, device=device, seed=0, env_offset=lo, **env_kw)
+    venv.reset()
+    gen = torch.Generator(device=device)
+    gen.manual_seed(12345 + rank)
+    n_act = args.warmup + args.steps
+    actions = torch.randint(0, 3, (n_act, hi - lo, S), generator=gen, device=device, dtype=torch.int8)
+
+    for t in range(args.warmup):
+        venv.step(actions[t])
+    torch.cuda.synchronize(device)
+
+    stream = torch.cuda.current_stream(device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    episodes = torch.zeros((), dtype=torch.int64, device=device)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for t in range(args.steps):
+        ev[t][0].record(stream)
+        _, _, _, info = venv.step(actions[args.warmup + t])
+        ev[t][1].record(stream)
+    torch.cuda.synchronize(device)
+    if distributed:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    episodes += info['episode_done'].sum()
+
+    if distributed:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        km = torch.tensor([kern_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kern_ms = float(km.item())
+
+    lay = venv.layout
+    B = algorithmic_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
+    achieved = B * (hi - lo) / (kern_ms * 1e-3) / 1e9
+    value = n_total * args.steps / elapsed
+    workload = (f'cfg3: {per} envs/GPU x (20x20, 4 snakes, vision_range=5, frame_stack=1), '
+                'random actions, all-done auto-reset in the step'
+                if (args.height, args.width, S, args.vision_range, args.frame_stack) == (20, 20, 4, 5, 1)
+                else f'{per} envs/GPU x ({args.height}x{args.width}, {S} snakes, '
+                     f'vision_range={args.vision_range}, frame_stack={args.frame_stack})')
+    traffic = None
+    pmc_path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            key = f'{args.height}x{args.width}_S{S}_vr{args.vision_range}_fs{args.frame_stack}_N{hi - lo}'
+            if key in pm:
+                traffic = pm[key]['hbm_bytes_per_launch']
+        except (OSError, ValueError, KeyError):
+            traffic = None
+    line = {
+        'metric': METRIC,
+        'value': round(value, 1),
+        'unit': 'env-steps/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'u8',
+        'data': 'synthetic (uniform random actions, seeded MT19937 envs)',
+        'config': {'workload': workload, 'num_envs': n_total, 'envs_per_gpu': per,
+                   'height': args.height, 'width': args.width, 'num_snakes': S,
+                   'vision_range': args.vision_range, 'frame_stack': args.frame_stack,
+                   'snake_length': 3, 'parallelism': f'env-shard x{world}'},
+        'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
+                     'traffic': traffic, 'algorithmic_bytes_per_env_step': B,
+                     'kernel_ms': round(kern_ms, 4)},
+        'cpu_baseline': None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_baseline(env_kw, S, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

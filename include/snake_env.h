@@ -1,0 +1,131 @@
+/*
+ * snake_env.h -- C-ABI of the MI355X-native batched multi-snake environment.
+ *
+ * The drop-in boundary for the reference's hot path (tranthai189765/MARL-Snake,
+ * marlenv/marlenv/envs/snake_env.py SnakeEnv.reset/step, reached through
+ * marlenv/marlenv/wrappers.py make_snake). The reference is pure Python, so its
+ * "FFI" for this path is the Python method surface; the product's Python host
+ * layer (marl-snake_amd/marlenv) binds these entry points with ctypes
+ * (marl-snake_amd/marlenv/_native.py) and re-exposes make_snake()/reset()/step().
+ *
+ * Conventions
+ *   - plain C types only; every buffer pointer is DEVICE memory allocated and
+ *     owned by the caller (PyTorch); the library allocates nothing on the device.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream); calls
+ *     are stream-ordered and asynchronous; not re-entrant per state.
+ *   - return 0 on success, a negative SNAKE_E* code on a bad argument (message in
+ *     snake_last_error()), never abort.
+ *   - env i of a batch is a standalone reference SnakeEnv after
+ *     np.random.seed(base_seed + env_offset + i).
+ */
+#ifndef SNAKE_ENV_H
+#define SNAKE_ENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SNAKE_ABI_VERSION 1
+
+#define SNAKE_OK           0
+#define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
+#define SNAKE_E_ARG       -2   /* NULL / mis-sized buffer, num_envs out of range */
+#define SNAKE_E_LAUNCH    -3   /* HIP launch error (message has hipGetErrorString) */
+
+/* Environment configuration. Mirrors SnakeEnv.__init__ kwargs
+ * (snake_env.py:58-129) and the gym ids of envs/__init__.py:3-16. */
+typedef struct {
+    int32_t height, width;      /* grid incl. walls, 3..255 */
+    int32_t num_snakes;         /* S, 1..16 */
+    int32_t snake_length;       /* initial length L >= 2 */
+    int32_t vision_range;       /* 0 == None (full-map obs), else crop (2vr+1)^2 */
+    int32_t frame_stack;        /* fs >= 1, obs channels = 8*fs */
+    int32_t observer;           /* 0 = 'snake' (actions 0/1/2), 1 = 'human' (0..4) */
+    int32_t num_fruits;         /* 1..64; default round(0.8*S) (:87-88) */
+    double  rew_fruit, rew_kill, rew_lose, rew_win, rew_time;   /* reward_dict */
+    double  max_episode_steps;  /* 1e4 by default (:56) */
+    int32_t coop;               /* 1 = SnakeCoop-v1: episode ends when ANY snake dies */
+    int32_t autoreset;          /* 1 = reset an env inside snake_step when all its dones
+                                   are True and return the reset obs (vector-env semantics,
+                                   wrappers.py:139-145); 0 = return the terminal obs */
+} snake_cfg;
+
+/* Byte sizes of every caller-allocated buffer for num_envs envs (snake_plan). */
+typedef struct {
+    int64_t grid;       /* uint8  [N][fs][grid_stride]   grid ring (newest = env[2]) */
+    int64_t snake;      /* int32  [N][S][4]              packed snake records */
+    int64_t body;       /* uint8  [N][S][ring_cap]       direction deques (rings) */
+    int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos */
+    int64_t stats;      /* double [N][4][S]              episode scores/steps/fruits/kills */
+    int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
+    int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
+    int64_t jscratch;   /* uint16 [N][n_cand] reset scratch, 0 when it fits in LDS */
+    int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */
+    int64_t rew;        /* double [N][S] */
+    int64_t done;       /* uint8  [N][S] */
+    int64_t ep_done;    /* uint8  [N]                    1 when the step ended the episode */
+    int64_t rank;       /* int32  [N][S]                 info['rank'] (valid where ep_done) */
+    int64_t ep_stats;   /* double [N][4][S]              info episode_* (valid where ep_done) */
+    int64_t err;        /* int32  [N]                    1 = invalid action (reference KeyError) */
+    int64_t n_cand;     /* rows of the spawn-pose table */
+    int32_t obs_h, obs_w, obs_c;
+    int32_t grid_stride, ring_cap;
+} snake_layout;
+
+typedef struct {        /* device state buffers (layouts in snake_layout) */
+    uint8_t  *grid;
+    int32_t  *snake;
+    uint8_t  *body;
+    int32_t  *env;
+    double   *stats;
+    uint32_t *mt;
+    const int16_t *cand;
+    uint16_t *jscratch; /* may be NULL when layout.jscratch == 0 */
+} snake_state;
+
+typedef struct {        /* device output buffers of one step/reset */
+    uint8_t *obs;
+    double  *rew;
+    uint8_t *done;
+    uint8_t *ep_done;
+    int32_t *rank;
+    double  *ep_stats;
+    int32_t *err;
+} snake_out;
+
+/* Validate cfg and compute buffer sizes. Replaces SnakeEnv.__init__'s checks and
+ * observation_space shape (snake_env.py:58-129). */
+int snake_plan(const snake_cfg *cfg, int64_t num_envs, snake_layout *out);
+
+/* Host-side spawn-pose table = dfs_sweep_empty(make_grid(H, W), L) in reference
+ * order (grid_util.py:73-115), as int16 cell indices r*W+c, n_cand x L. Static per
+ * (H, W, L): computed once, uploaded once. Returns n_cand, or < 0. */
+int64_t snake_build_candidates(const snake_cfg *cfg, int16_t *host_out, int64_t capacity);
+
+/* Seed env i's MT19937 with base_seed + env_offset + i (np.random.seed,
+ * snake_env.py:581 / grid_util.py:130 use the global legacy RandomState). */
+int snake_seed(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
+               uint32_t base_seed, int64_t env_offset, void *stream);
+
+/* SnakeEnv.reset() (snake_env.py:131-159) for every env whose env_mask byte is
+ * nonzero (env_mask == NULL: all envs); writes out->obs for those envs. */
+int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
+                const uint8_t *env_mask, const snake_out *out, void *stream);
+
+/* SnakeEnv.step(actions) (snake_env.py:301-414) for all envs at once; actions is
+ * int8 [N][S]. With cfg->autoreset an env whose dones are all True is reset in
+ * the same launch and its out->obs holds the reset observation. */
+int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
+               const int8_t *actions, const snake_out *out, void *stream);
+
+/* Last error message of this thread ("" if none). */
+const char *snake_last_error(void);
+
+int snake_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SNAKE_ENV_H */

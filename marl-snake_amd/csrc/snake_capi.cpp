@@ -1,0 +1,356 @@
+// snake_capi.cpp -- C-ABI entry points (include/snake_env.h): config validation,
+// buffer planning, the static spawn-pose table and argument checks before the
+// HIP launches in snake_kernels.hip.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "snake_internal.h"
+
+namespace snake {
+
+static thread_local char g_err[512];
+
+void set_error(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+static int pow2_at_least(int x)
+{
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// SnakeEnv.__init__ argument rules (snake_env.py:58-129) plus this
+// implementation's static limits (documented in DESIGN.md).
+static int check_cfg(const snake_cfg *c)
+{
+    if (!c) { set_error("cfg is NULL"); return SNAKE_E_CONFIG; }
+    if (c->height < 3 || c->height > 255 || c->width < 3 || c->width > 255) {
+        set_error("height/width must be in [3, 255] (got %d x %d)", c->height, c->width);
+        return SNAKE_E_CONFIG;
+    }
+    if (c->num_snakes < 1 || c->num_snakes > kMaxSnakes) {
+        set_error("num_snakes must be in [1, %d] (got %d)", kMaxSnakes, c->num_snakes);
+        return SNAKE_E_CONFIG;
+    }
+    if (c->snake_length < 2 || c->snake_length > 63) {
+        // Snake.__init__ asserts len(coords) > 1 (core/snake.py:54)
+        set_error("snake_length must be in [2, 63] (got %d)", c->snake_length);
+        return SNAKE_E_CONFIG;
+    }
+    if (c->snake_length * c->num_snakes > kWave) {
+        set_error("num_snakes * snake_length must be <= 64 (got %d)", c->snake_length * c->num_snakes);
+        return SNAKE_E_CONFIG;
+    }
+    if (c->vision_range < 0 || 2 * c->vision_range + 1 > 255) {
+        set_error("vision_range must be None/0 or in [1, 127] (got %d)", c->vision_range);
+        return SNAKE_E_CONFIG;
+    }
+    if (c->frame_stack < 1 || c->frame_stack > 16) {
+        set_error("frame_stack must be in [1, 16] (got %d)", c->frame_stack);
+        return SNAKE_E_CONFIG;
+    }
+    if (c->observer != 0 && c->observer != 1) {
+        set_error("observer must be 'snake' or 'human'");
+        return SNAKE_E_CONFIG;
+    }
+    if (c->num_fruits < 1 || c->num_fruits > kMaxFruits) {
+        // num_fruits == 0 makes the reference paint the whole grid FRUIT
+        // (grid[None, None] = 2 at snake_env.py:147-148): not supported.
+        set_error("num_fruits must be in [1, %d] (got %d)", kMaxFruits, c->num_fruits);
+        return SNAKE_E_CONFIG;
+    }
+    int interior = (c->height - 2) * (c->width - 2);
+    if (interior < c->num_snakes * c->snake_length + 1) {
+        set_error("grid too small for %d snakes of length %d", c->num_snakes, c->snake_length);
+        return SNAKE_E_CONFIG;
+    }
+    return SNAKE_OK;
+}
+
+// ---- spawn-pose table: dfs_sweep_empty(make_grid(H, W), L), grid_util.py:73-115.
+// Paths are self-avoiding walks of L empty cells, head = first cell, extended in
+// SHIFTS order (0,+1),(+1,0),(0,-1),(-1,0) (grid_util.py:7-11); a walk is kept only
+// while its head has a free neighbour outside the walk (_head_blocked). Iterative
+// DFS; emits int16 cell indices r*W+c.
+struct Dfs {
+    int H, W, L;
+    std::vector<uint8_t> empty;
+    std::vector<int16_t> *out;
+    int64_t count = 0;
+    int path[64];
+    int dir_state[64];
+};
+
+static bool in_path(const Dfs &d, int n, int cell)
+{
+    for (int i = 0; i < n; i++)
+        if (d.path[i] == cell) return true;
+    return false;
+}
+
+static bool head_blocked(const Dfs &d, int n, int extra)
+{
+    static const int dr[4] = {0, 1, 0, -1}, dc[4] = {1, 0, -1, 0};
+    int hr = d.path[0] / d.W, hc = d.path[0] % d.W, blocked = 0;
+    for (int s = 0; s < 4; s++) {
+        int r = hr + dr[s], c = hc + dc[s];
+        int cell = r * d.W + c;
+        if (r < 0 || c < 0 || r >= d.H || c >= d.W || !d.empty[cell] || in_path(d, n, cell) ||
+            cell == extra)
+            blocked++;
+    }
+    return blocked == 4;
+}
+
+static void dfs_from(Dfs &d, int start)
+{
+    static const int dr[4] = {0, 1, 0, -1}, dc[4] = {1, 0, -1, 0};
+    int n = 1;
+    d.path[0] = start;
+    d.dir_state[0] = 0;
+    if (d.L == 1) { d.count++; return; }
+    while (n > 0) {
+        if (n == d.L) {  // complete walk
+            if (d.out) d.out->insert(d.out->end(), d.path, d.path + d.L);
+            d.count++;
+            n--;
+            continue;
+        }
+        int &s = d.dir_state[n - 1];
+        if (s >= 4) { n--; continue; }
+        int cur = d.path[n - 1];
+        int r = cur / d.W + dr[s], c = cur % d.W + dc[s];
+        s++;
+        if (r < 0 || c < 0 || r >= d.H || c >= d.W) continue;
+        int cell = r * d.W + c;
+        if (!d.empty[cell] || in_path(d, n, cell)) continue;
+        if (head_blocked(d, n, cell)) continue;
+        d.path[n] = cell;
+        d.dir_state[n] = 0;
+        n++;
+    }
+}
+
+static int64_t build_table(int H, int W, int L, std::vector<int16_t> *out)
+{
+    Dfs d;
+    d.H = H; d.W = W; d.L = L;
+    d.empty.assign((size_t)H * W, 0);
+    for (int r = 1; r < H - 1; r++)
+        for (int c = 1; c < W - 1; c++) d.empty[(size_t)r * W + c] = 1;  // make_grid :14-20
+    d.out = out;
+    for (int cell = 0; cell < H * W; cell++)
+        if (d.empty[cell]) dfs_from(d, cell);
+    return d.count;
+}
+
+// n_cand per (H, W, L), memoised: snake_step/snake_reset re-plan on every call.
+static int64_t cached_count(int H, int W, int L)
+{
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int>, int64_t> memo;
+    std::lock_guard<std::mutex> lock(mu);
+    auto key = std::make_tuple(H, W, L);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+    int64_t n = build_table(H, W, L, nullptr);
+    memo[key] = n;
+    return n;
+}
+
+int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
+{
+    int rc = check_cfg(c);
+    if (rc) return rc;
+    if (N < 1 || N > (int64_t)1 << 26) {
+        set_error("num_envs must be in [1, 2^26] (got %lld)", (long long)N);
+        return SNAKE_E_ARG;
+    }
+    memset(o, 0, sizeof *o);
+    const int64_t S = c->num_snakes, fs = c->frame_stack, HW = (int64_t)c->height * c->width;
+    const int oh = c->vision_range ? 2 * c->vision_range + 1 : c->height;
+    const int ow = c->vision_range ? 2 * c->vision_range + 1 : c->width;
+    o->grid_stride = (int32_t)round_up(HW, 16);
+    o->ring_cap = pow2_at_least((c->height - 2) * (c->width - 2));
+    o->n_cand = cached_count(c->height, c->width, c->snake_length);
+    o->obs_h = oh; o->obs_w = ow; o->obs_c = 8 * c->frame_stack;
+    o->grid = N * fs * o->grid_stride;
+    o->snake = N * S * 4 * 4;
+    o->body = N * S * o->ring_cap;
+    o->env = N * kEnvRec * 4;
+    o->stats = N * 4 * S * 8;
+    o->mt = N * kMtN * 4;
+    o->cand = o->n_cand * c->snake_length * 2;
+    o->jscratch = (o->n_cand * 2 <= kJarrLdsMax) ? 0 : N * o->n_cand * 2;
+    o->obs = N * S * oh * ow * 8 * fs;
+    o->rew = N * S * 8;
+    o->done = N * S;
+    o->ep_done = N;
+    o->rank = N * S * 4;
+    o->ep_stats = N * 4 * S * 8;
+    o->err = N * 4;
+    if (o->n_cand > 65535) {
+        set_error("%lld spawn poses: more than the 65535 the reset scratch indexes",
+                  (long long)o->n_cand);
+        return SNAKE_E_CONFIG;
+    }
+    if (o->n_cand < S) {
+        set_error("only %lld spawn poses for %lld snakes", (long long)o->n_cand, (long long)S);
+        return SNAKE_E_CONFIG;
+    }
+    return SNAKE_OK;
+}
+
+int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
+{
+    snake_layout lay;
+    int rc = layout_of(c, N, &lay);
+    if (rc) return rc;
+    if (n_cand != lay.n_cand) {
+        set_error("spawn-pose table has %lld rows, expected %lld", (long long)n_cand,
+                  (long long)lay.n_cand);
+        return SNAKE_E_ARG;
+    }
+    memset(k, 0, sizeof *k);
+    k->N = (int)N;
+    k->H = c->height; k->W = c->width; k->HW = c->height * c->width;
+    k->S = c->num_snakes; k->L = c->snake_length; k->vr = c->vision_range;
+    k->fs = c->frame_stack; k->observer = c->observer; k->num_fruits = c->num_fruits;
+    k->coop = c->coop ? 1 : 0; k->autoreset = c->autoreset ? 1 : 0;
+    k->oh = lay.obs_h; k->ow = lay.obs_w;
+    k->units = k->S * k->oh * k->ow * k->fs;
+    k->grid_stride = lay.grid_stride; k->ring_cap = lay.ring_cap; k->n_cand = (int)lay.n_cand;
+    k->cs = (k->HW + kWave - 1) / kWave;
+    // 128 units in mixed radix (f: fs, j: ow, i: oh, k: S)
+    int64_t a = 128;
+    k->adv_f = (int)(a % k->fs); a /= k->fs;
+    k->adv_j = (int)(a % k->ow); a /= k->ow;
+    k->adv_i = (int)(a % k->oh); a /= k->oh;
+    k->adv_k = (int)a;
+    int off = 0;
+    k->lds_frames = off; off += (int)round_up((int64_t)k->fs * k->grid_stride, 16);
+    k->lds_centers = off; off += (int)round_up(4 * k->fs * kMaxSnakes, 16);
+    k->lds_fruit = off; off += (int)round_up(2 * kMaxFruits, 16);
+    k->jarr_in_lds = lay.jscratch == 0;
+    k->lds_jarr = off;
+    if (k->jarr_in_lds) off += (int)round_up(2 * (int64_t)k->n_cand, 16);
+    k->lds_bytes = off;
+    k->rf = c->rew_fruit; k->rk = c->rew_kill; k->rl = c->rew_lose; k->rw = c->rew_win;
+    k->rt = c->rew_time; k->max_steps = c->max_episode_steps;
+    return SNAKE_OK;
+}
+
+static int check_state(const KCfg &k, const snake_state *st, bool need_all)
+{
+    if (!st || !st->grid || !st->snake || !st->body || !st->env || !st->stats || !st->mt ||
+        !st->cand) {
+        set_error("snake_state has a NULL buffer");
+        return SNAKE_E_ARG;
+    }
+    if (!k.jarr_in_lds && !st->jscratch) {
+        set_error("snake_state.jscratch is required for this config (n_cand=%d)", k.n_cand);
+        return SNAKE_E_ARG;
+    }
+    (void)need_all;
+    return SNAKE_OK;
+}
+
+static int check_out(const snake_out *o, bool step)
+{
+    if (!o || !o->obs) { set_error("snake_out.obs is NULL"); return SNAKE_E_ARG; }
+    if (step && (!o->rew || !o->done || !o->ep_done || !o->rank || !o->ep_stats || !o->err)) {
+        set_error("snake_out has a NULL step buffer");
+        return SNAKE_E_ARG;
+    }
+    return SNAKE_OK;
+}
+
+static int64_t n_cand_of(const snake_cfg *c)
+{
+    snake_layout lay;
+    if (layout_of(c, 1, &lay)) return -1;
+    return lay.n_cand;
+}
+
+}  // namespace snake
+
+using namespace snake;
+
+extern "C" {
+
+int snake_abi_version(void) { return SNAKE_ABI_VERSION; }
+
+const char *snake_last_error(void) { return g_err; }
+
+int snake_plan(const snake_cfg *cfg, int64_t num_envs, snake_layout *out)
+{
+    if (!out) { set_error("out is NULL"); return SNAKE_E_ARG; }
+    g_err[0] = 0;
+    return layout_of(cfg, num_envs, out);
+}
+
+int64_t snake_build_candidates(const snake_cfg *cfg, int16_t *host_out, int64_t capacity)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    std::vector<int16_t> v;
+    int64_t n = build_table(cfg->height, cfg->width, cfg->snake_length, &v);
+    if (host_out) {
+        if (capacity < (int64_t)v.size()) {
+            set_error("capacity %lld < %lld table entries", (long long)capacity, (long long)v.size());
+            return SNAKE_E_ARG;
+        }
+        memcpy(host_out, v.data(), v.size() * sizeof(int16_t));
+    }
+    return n;
+}
+
+int snake_seed(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, uint32_t base_seed,
+               int64_t env_offset, void *stream)
+{
+    KCfg k;
+    int rc = build_kcfg(cfg, num_envs, n_cand_of(cfg), &k);
+    if (rc) return rc;
+    if ((rc = check_state(k, st, false))) return rc;
+    if (env_offset < 0) { set_error("env_offset < 0"); return SNAKE_E_ARG; }
+    return launch_seed(k, *st, base_seed, env_offset, stream);
+}
+
+int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
+                const uint8_t *env_mask, const snake_out *out, void *stream)
+{
+    KCfg k;
+    int rc = build_kcfg(cfg, num_envs, n_cand_of(cfg), &k);
+    if (rc) return rc;
+    if ((rc = check_state(k, st, true))) return rc;
+    if ((rc = check_out(out, false))) return rc;
+    return launch_reset(k, *st, env_mask, *out, stream);
+}
+
+int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, const int8_t *actions,
+               const snake_out *out, void *stream)
+{
+    KCfg k;
+    int rc = build_kcfg(cfg, num_envs, n_cand_of(cfg), &k);
+    if (rc) return rc;
+    if ((rc = check_state(k, st, true))) return rc;
+    if ((rc = check_out(out, true))) return rc;
+    if (!actions) { set_error("actions is NULL"); return SNAKE_E_ARG; }
+    return launch_step(k, *st, actions, *out, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,46 @@
+// snake_internal.h -- launch-side configuration shared by snake_capi.cpp and
+// snake_kernels.hip (not part of the C-ABI).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/snake_env.h"
+
+namespace snake {
+
+constexpr int kWave = 64;
+constexpr int kMtN = 624;
+constexpr int kMaxSnakes = 16;
+constexpr int kMaxFruits = 64;
+constexpr int kEnvRec = 8;          // int32 words per env record
+constexpr int kJarrLdsMax = 16384;  // bytes of reset scratch kept in LDS
+
+// env record words
+enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3 };
+
+// Everything a kernel needs, by value (a kernel argument).
+struct KCfg {
+    int N;
+    int H, W, HW, S, L, vr, fs, observer, num_fruits, coop, autoreset;
+    int oh, ow, units;          // units = S*oh*ow*fs (one unit = 8 obs bytes)
+    int grid_stride, ring_cap, n_cand;
+    int cs;                     // cells per lane when a wave sweeps the grid
+    // step of 128 units expressed in the mixed radix (fs, ow, oh, S)
+    int adv_f, adv_j, adv_i, adv_k;
+    // dynamic LDS carve (bytes, 16-aligned)
+    int lds_frames, lds_centers, lds_fruit, lds_jarr, lds_bytes, jarr_in_lds;
+    double rf, rk, rl, rw, rt, max_steps;
+};
+
+int build_kcfg(const snake_cfg *c, int64_t num_envs, int64_t n_cand, KCfg *k);
+int layout_of(const snake_cfg *c, int64_t num_envs, snake_layout *out);
+void set_error(const char *fmt, ...);
+
+// launchers (snake_kernels.hip)
+int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_t env_offset,
+                void *stream);
+int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, const snake_out &o,
+                 void *stream);
+int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, const snake_out &o,
+                void *stream);
+
+}  // namespace snake

@@ -1,0 +1,89 @@
+"""ctypes binding of libsnake_amd.so (C-ABI declared in include/snake_env.h).
+
+The product has no CPU fallback: if the HIP library is missing or fails to
+load, every env constructor raises. Build it with ``python __graft_entry__.py``
+(or ``make -C marl-snake_amd/csrc``).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
+
+SNAKE_ABI_VERSION = 1
+
+# Symbols include/snake_env.h declares (checked by tests/test_capi.py).
+EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
+           'snake_last_error', 'snake_abi_version')
+
+
+class SnakeCfg(ctypes.Structure):
+    _fields_ = [('height', ctypes.c_int32), ('width', ctypes.c_int32),
+                ('num_snakes', ctypes.c_int32), ('snake_length', ctypes.c_int32),
+                ('vision_range', ctypes.c_int32), ('frame_stack', ctypes.c_int32),
+                ('observer', ctypes.c_int32), ('num_fruits', ctypes.c_int32),
+                ('rew_fruit', ctypes.c_double), ('rew_kill', ctypes.c_double),
+                ('rew_lose', ctypes.c_double), ('rew_win', ctypes.c_double),
+                ('rew_time', ctypes.c_double), ('max_episode_steps', ctypes.c_double),
+                ('coop', ctypes.c_int32), ('autoreset', ctypes.c_int32)]
+
+
+class SnakeLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        'grid', 'snake', 'body', 'env', 'stats', 'mt', 'cand', 'jscratch', 'obs', 'rew', 'done',
+        'ep_done', 'rank', 'ep_stats', 'err', 'n_cand')] + [
+        ('obs_h', ctypes.c_int32), ('obs_w', ctypes.c_int32), ('obs_c', ctypes.c_int32),
+        ('grid_stride', ctypes.c_int32), ('ring_cap', ctypes.c_int32)]
+
+
+class SnakeState(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        'grid', 'snake', 'body', 'env', 'stats', 'mt', 'cand', 'jscratch')]
+
+
+class SnakeOut(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        'obs', 'rew', 'done', 'ep_done', 'rank', 'ep_stats', 'err')]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libsnake_amd.so once; raise loudly when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f'{LIB_PATH} not built: run `python __graft_entry__.py` '
+                          '(hipcc --offload-arch=gfx950); there is no CPU fallback')
+    L = ctypes.CDLL(LIB_PATH)
+    P, I64 = ctypes.c_void_p, ctypes.c_int64
+    L.snake_abi_version.restype = ctypes.c_int
+    L.snake_last_error.restype = ctypes.c_char_p
+    L.snake_plan.argtypes = [ctypes.POINTER(SnakeCfg), I64, ctypes.POINTER(SnakeLayout)]
+    L.snake_build_candidates.restype = I64
+    L.snake_build_candidates.argtypes = [ctypes.POINTER(SnakeCfg), P, I64]
+    L.snake_seed.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64,
+                             ctypes.c_uint32, I64, P]
+    L.snake_reset.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P,
+                              ctypes.POINTER(SnakeOut), P]
+    L.snake_step.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P,
+                             ctypes.POINTER(SnakeOut), P]
+    if L.snake_abi_version() != SNAKE_ABI_VERSION:
+        raise NativeError('libsnake_amd.so ABI version mismatch; rebuild it')
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc < 0:
+        msg = lib().snake_last_error().decode(errors='replace')
+        if rc == -1:
+            raise ValueError(msg)
+        raise NativeError(f'snake C-ABI error {rc}: {msg}')
+    return rc

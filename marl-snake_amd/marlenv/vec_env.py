@@ -1,0 +1,223 @@
+"""SnakeVecEnv: N independent SnakeEnv instances stepped by one HIP launch.
+
+Replaces the reference's process-level vectorisation (gym AsyncVectorEnv over
+forked SnakeEnv workers, marlenv/marlenv/wrappers.py:203-223) with one
+64-lane wavefront per env on the GPU. State and outputs are PyTorch-ROCm
+tensors; the kernels are reached through the C-ABI of include/snake_env.h.
+
+Semantics per env are exactly the reference SnakeEnv's (bit-identical grids,
+dones and float64 rewards); env i uses its own MT19937 seeded with
+``seed + env_offset + i`` (np.random.seed semantics), so a shard of a larger
+batch reproduces the same trajectories as the full batch.
+
+Auto-reset (``autoreset=True``, the default): when every done of an env is True
+the env is reset inside the same launch and the returned obs is the reset
+observation, while rewards/dones/info are the terminal ones -- the worker
+semantics of wrappers.py:139-145 (reset on ``all(done)``).
+"""
+import ctypes
+
+import numpy as np
+
+from . import spaces
+from ._native import SnakeLayout, SnakeOut, SnakeState, check, lib
+from .config import build_cfg
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class SnakeVecEnv:
+    def __init__(self, num_envs, num_snakes=4, device=None, seed=0, env_offset=0,
+                 autoreset=True, coop=False, strict=False, **env_kwargs):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError('SnakeVecEnv needs a HIP device (MI355X); there is no CPU fallback')
+        self.num_envs = N = int(num_envs)
+        self.cfg, self.meta = build_cfg(num_snakes=num_snakes, coop=coop, autoreset=autoreset,
+                                        **env_kwargs)
+        self.num_snakes = S = self.cfg.num_snakes
+        self.autoreset = bool(autoreset)
+        self.strict = bool(strict)
+        self.seed_base = int(seed) & 0xffffffff
+        self.env_offset = int(env_offset)
+        L = lib()
+        lay = SnakeLayout()
+        check(L.snake_plan(ctypes.byref(self.cfg), N, ctypes.byref(lay)))
+        self.layout = lay
+        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        dev = self.device
+        self.obs_shape = (S, lay.obs_h, lay.obs_w, lay.obs_c)
+        self.grid_shape = (self.cfg.height, self.cfg.width)
+        self.action_n = 5 if self.cfg.observer == 1 else 3
+
+        def buf(nbytes, dtype=torch.uint8):
+            return torch.zeros(max(int(nbytes), 16), dtype=torch.uint8, device=dev).view(dtype)
+
+        # state (layouts: include/snake_env.h snake_layout)
+        self.grid = buf(lay.grid)
+        self.snake = buf(lay.snake, torch.int32)
+        self.body = buf(lay.body)
+        self.env_rec = buf(lay.env, torch.int32)
+        self.stats = buf(lay.stats, torch.float64)
+        self.mt = buf(lay.mt, torch.int32)
+        self.jscratch = buf(lay.jscratch, torch.int16) if lay.jscratch else None
+        cap = int(lay.n_cand) * self.cfg.snake_length
+        host = np.zeros(cap, np.int16)
+        n = check(L.snake_build_candidates(ctypes.byref(self.cfg), host.ctypes.data_as(ctypes.c_void_p), cap))
+        assert n == lay.n_cand
+        self.cand = torch.from_numpy(host).to(dev)
+        self._state = SnakeState(
+            self.grid.data_ptr(), self.snake.data_ptr(), self.body.data_ptr(), self.env_rec.data_ptr(),
+            self.stats.data_ptr(), self.mt.data_ptr(), self.cand.data_ptr(),
+            self.jscratch.data_ptr() if self.jscratch is not None else None)
+        check(L.snake_seed(ctypes.byref(self.cfg), ctypes.byref(self._state), N, self.seed_base,
+                           self.env_offset, self._stream()))
+
+        self.single_action_space = spaces.Discrete(self.action_n)
+        self.single_observation_space = spaces.Box(0, 255, self.obs_shape, np.uint8)
+        self.observation_space = spaces.Box(0, 255, (N,) + self.obs_shape, np.uint8)
+        self.action_space = spaces.Box(0, self.action_n - 1, (N, S), np.int64)
+        self._reset_done = False
+
+    # ------------------------------------------------------------------ utils
+    def _stream(self):
+        torch = _torch()
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _new_out(self):
+        torch = _torch()
+        N, S = self.num_envs, self.num_snakes
+        d = self.device
+        out = dict(
+            obs=torch.empty((N,) + self.obs_shape, dtype=torch.uint8, device=d),
+            rew=torch.empty((N, S), dtype=torch.float64, device=d),
+            done=torch.empty((N, S), dtype=torch.bool, device=d),
+            ep_done=torch.empty((N,), dtype=torch.bool, device=d),
+            rank=torch.empty((N, S), dtype=torch.int32, device=d),
+            ep_stats=torch.empty((N, 4, S), dtype=torch.float64, device=d),
+            err=torch.empty((N,), dtype=torch.int32, device=d))
+        so = SnakeOut(*(out[k].data_ptr() for k in ('obs', 'rew', 'done', 'ep_done', 'rank', 'ep_stats', 'err')))
+        return out, so
+
+    def _actions(self, actions):
+        torch = _torch()
+        a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions))
+        a = a.to(self.device)
+        if a.dtype != torch.int8:
+            if a.dtype.is_floating_point:
+                bad = a != torch.floor(a)
+                a = torch.where(bad, torch.full_like(a, -1), a)
+            a = a.clamp(-128, 127).to(torch.int8)
+        a = a.reshape(self.num_envs, self.num_snakes).contiguous()
+        return a
+
+    # ------------------------------------------------------------------- API
+    def reset(self, mask=None):
+        """SnakeEnv.reset (snake_env.py:131-159) for all envs, or those where mask is True.
+        Returns the (N, S, h, w, 8*fs) uint8 observation tensor (rows of envs not in
+        mask are left uninitialised)."""
+        torch = _torch()
+        out, so = self._new_out()
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).reshape(self.num_envs).contiguous()
+        check(lib().snake_reset(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+                                ctypes.c_void_p(m.data_ptr()) if m is not None else None,
+                                ctypes.byref(so), self._stream()))
+        self._keep = m
+        self._reset_done = True
+        return out['obs']
+
+    def step(self, actions):
+        """SnakeEnv.step (snake_env.py:301-414) for every env.
+
+        actions: (N, S) ints ({0,1,2} for observer='snake', {0..4} for 'human').
+        Returns (obs uint8 (N,S,h,w,C), rewards float64 (N,S), dones bool (N,S), info)
+        with info tensors 'episode_done' (N,), 'rank' (N,S) and 'episode_scores',
+        'episode_steps', 'episode_fruits', 'episode_kills' (N,S), meaningful where
+        episode_done; 'error' (N,) flags envs whose step was rejected for an invalid
+        action (the reference's KeyError; such an env is left unchanged).
+        All outputs are freshly allocated every call."""
+        if not self._reset_done:
+            raise RuntimeError('call reset() before step()')
+        a = self._actions(actions)
+        out, so = self._new_out()
+        check(lib().snake_step(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+                               ctypes.c_void_p(a.data_ptr()), ctypes.byref(so), self._stream()))
+        self._keep = a
+        info = {'episode_done': out['ep_done'], 'rank': out['rank'],
+                'episode_scores': out['ep_stats'][:, 0], 'episode_steps': out['ep_stats'][:, 1],
+                'episode_fruits': out['ep_stats'][:, 2], 'episode_kills': out['ep_stats'][:, 3],
+                'error': out['err']}
+        if self.strict and bool(out['err'].any()):
+            bad = out['err'].nonzero().flatten().tolist()
+            raise KeyError(f'invalid action for an alive snake in envs {bad[:8]}')
+        return out['obs'], out['rew'], out['done'], info
+
+    # --------------------------------------------------------- introspection
+    def grids(self):
+        """Current grid of every env, (N, H, W) int8 (newest ring slot)."""
+        torch = _torch()
+        lay, fs = self.layout, self.cfg.frame_stack
+        H, W = self.grid_shape
+        ring = self.grid.view(self.num_envs, fs, lay.grid_stride)
+        cur = self.env_rec.view(self.num_envs, 8)[:, 2].long()
+        g = ring[torch.arange(self.num_envs, device=self.device), cur][:, :H * W]
+        return g.reshape(self.num_envs, H, W).view(torch.int8)
+
+    def alive_counters(self):
+        return self.env_rec.view(self.num_envs, 8)[:, 0]
+
+    def episode_lengths(self):
+        return self.env_rec.view(self.num_envs, 8)[:, 1]
+
+    def snake_table(self):
+        """(N, S, 7) int32: head r,c, tail r,c, dir (0 UP,1 RIGHT,2 DOWN,3 LEFT), alive, length."""
+        torch = _torch()
+        r = self.snake.view(self.num_envs, self.num_snakes, 4)
+        x, y, z = r[..., 0], r[..., 1], r[..., 2]
+        return torch.stack([x & 255, (x >> 8) & 255, (x >> 16) & 255, (x >> 24) & 255,
+                            y & 3, (y >> 8) & 1, ((z >> 16) & 0xffff) + 1], dim=-1)
+
+    def mt_state(self):
+        """(N, 624) MT19937 keys (int32 view of uint32) and (N,) positions."""
+        return self.mt.view(self.num_envs, 624), self.env_rec.view(self.num_envs, 8)[:, 3]
+
+    def inject(self, i, grid, snakes, alive_snakes, episode_length=0):
+        """Overwrite env i with a crafted state (the env.grid / env.snakes assignment
+        the reference allows): grid (H, W) cell values, snakes = [(coords, alive)]
+        with coords [(r, c), ...] head first (core/snake.py:53-74). The frame
+        stack is refilled with this grid and the episode statistics are zeroed, as
+        _init_obs/_reset_epi_stats do; the env's MT19937 stream is left as is."""
+        torch = _torch()
+        H, W = self.grid_shape
+        S, fs, lay = self.num_snakes, self.cfg.frame_stack, self.layout
+        g = np.zeros(lay.grid_stride, np.uint8)
+        g[:H * W] = np.asarray(grid, np.int64).reshape(-1).astype(np.uint8)
+        ring = torch.from_numpy(np.tile(g, fs)).to(self.device)
+        self.grid.view(self.num_envs, fs * lay.grid_stride)[i].copy_(ring)
+        rec = np.zeros((S, 4), np.int32)
+        body = np.zeros((S, lay.ring_cap), np.uint8)
+        dmap = {(-1, 0): 0, (0, 1): 1, (1, 0): 2, (0, -1): 3}
+        for k, (coords, alive) in enumerate(snakes):
+            co = [tuple(int(x) for x in c) for c in coords]
+            dirs = [dmap[(a[0] - b[0], a[1] - b[1])] for a, b in zip(co[:-1], co[1:])]
+            body[k, :len(dirs)] = dirs
+            (hr, hc), (tr, tc) = co[0], co[-1]
+            x = hr | (hc << 8) | (tr << 16) | (tc << 24)
+            rec[k] = [x - (1 << 32) if x >= (1 << 31) else x, dirs[0] | (int(bool(alive)) << 8),
+                      (len(co) - 1) << 16, 0]
+        self.snake.view(self.num_envs, S * 4)[i].copy_(torch.from_numpy(rec.reshape(-1)).to(self.device))
+        self.body.view(self.num_envs, S * lay.ring_cap)[i].copy_(torch.from_numpy(body.reshape(-1)).to(self.device))
+        er = self.env_rec.view(self.num_envs, 8)
+        er[i, 0] = int(alive_snakes)
+        er[i, 1] = int(episode_length)
+        er[i, 2] = fs - 1
+        self.stats.view(self.num_envs, 4 * S)[i].zero_()
+        self._reset_done = True
+
+    def close(self):
+        pass

@@ -1,0 +1,92 @@
+"""make_snake and the agent wrappers (reference marlenv/marlenv/wrappers.py).
+
+make_snake(num_envs=1, ...) returns the single-env compat SnakeEnv wrapped in
+SingleMultiAgent (or SingleAgent when num_snakes == 1), as wrappers.py:203-223.
+make_snake(num_envs>1, ...) returns a SnakeVecEnv: all envs stepped by one HIP
+launch with all-done auto-reset (the reference forks one gym AsyncVectorEnv
+worker per env, wrappers.py:211-212); its outputs are torch tensors on the GPU.
+RenderGUI / AsyncVectorMultiEnv (OpenCV window, process pool) are out of scope.
+"""
+import numpy as np
+
+from . import spaces
+from .envs import REGISTRY, UNSUPPORTED
+from .vec_env import SnakeVecEnv
+
+
+class Wrapper:
+    def __init__(self, env):
+        self.env = env
+
+    def __getattr__(self, name):
+        if name.startswith('__'):
+            raise AttributeError(name)
+        return getattr(self.env, name)
+
+    @property
+    def unwrapped(self):
+        return getattr(self.env, 'unwrapped', self.env)
+
+    def reset(self, **kwargs):
+        return self.env.reset(**kwargs)
+
+    def step(self, action):
+        return self.env.step(action)
+
+    def close(self):
+        return self.env.close()
+
+
+class SingleAgent(Wrapper):                       # wrappers.py:84-105
+    def __init__(self, env):
+        super().__init__(env)
+        assert env.num_snakes == 1, 'Number of player must be one'
+        self.action_space = spaces.Discrete(len(self.env.action_dict))
+        if getattr(self.env, 'vision_range', None):
+            h = w = self.env.vision_range * 2 + 1
+            shape = (h, w, self.env.obs_ch)
+        else:
+            shape = (*self.env.grid_shape, self.env.obs_ch)
+        self.observation_space = spaces.Box(0, 255, shape, np.uint8)
+
+    def reset(self, **kwargs):
+        return self.env.reset(**kwargs)[0]
+
+    def step(self, action, **kwargs):
+        obs, rews, dones, infos = self.env.step([action], **kwargs)
+        return obs[0], rews[0], dones[0], {}
+
+
+class SingleMultiAgent(Wrapper):                  # wrappers.py:107-124
+    def __init__(self, env):
+        super().__init__(env)
+        self.action_space = spaces.Discrete(len(self.env.action_dict))
+        vision_range = getattr(self.env, 'vision_range', None)
+        obs_ch = getattr(self.env, 'obs_ch', 3)
+        if vision_range:
+            h = w = vision_range * 2 + 1
+            shape = (self.env.num_snakes, h, w, obs_ch)
+        else:
+            shape = (self.env.num_snakes, *self.env.grid_shape, obs_ch)
+        self.observation_space = spaces.Box(0, 255, shape, np.uint8)
+
+
+def make_snake(num_envs=1, num_snakes=4, env_id='Snake-v1', **kwargs):
+    """wrappers.py:203-223. Returns (env, None, None, properties)."""
+    if env_id in UNSUPPORTED:
+        raise NotImplementedError(f'{env_id} is not provided by the MI355X build (see DESIGN.md)')
+    if env_id not in REGISTRY:
+        raise KeyError(f'unknown env id {env_id!r}')
+    observer = kwargs.get('observer', 'snake')
+    action_n = 5 if observer == 'human' else 3
+    if num_envs > 1:
+        env = SnakeVecEnv(num_envs, num_snakes=num_snakes, coop=(env_id == 'SnakeCoop-v1'), **kwargs)
+    else:
+        env_wrapper = SingleMultiAgent if num_snakes > 1 else SingleAgent
+        env = env_wrapper(REGISTRY[env_id](num_snakes=num_snakes, **kwargs))
+    properties = {
+        'action_info': {'action_n': action_n},
+        'num_envs': num_envs,
+        'num_snakes': num_snakes,
+    }
+    return env, None, None, properties

@@ -1,0 +1,104 @@
+"""CPU checks of the product's C-ABI library (no GPU needed): it loads, exports
+every symbol include/snake_env.h declares, plans buffers, rejects bad configs
+the way SnakeEnv.__init__ does, and its host-side spawn-pose table equals the
+reference's dfs_sweep_empty order (golden digests)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import golden_io as G
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope='module')
+def native():
+    from marlenv import _native
+    if not os.path.exists(_native.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return _native
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, 'include', 'snake_env.h')).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'^\s*(?:const\s+)?\w+\s*\*?\s*(snake_\w+)\s*\(', src, flags=re.M)))
+
+
+def test_exports_match_header(native):
+    names = header_functions()
+    assert set(names) == set(native.EXPORTS), names
+    L = native.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    assert L.snake_abi_version() == native.SNAKE_ABI_VERSION
+
+
+def cfg(native, **kw):
+    from marlenv.config import build_cfg
+    return build_cfg(**kw)[0]
+
+
+def test_plan_sizes(native):
+    c = cfg(native, height=20, width=20, num_snakes=4, vision_range=5)
+    lay = native.SnakeLayout()
+    assert native.lib().snake_plan(ctypes.byref(c), 65536, ctypes.byref(lay)) == 0
+    assert (lay.obs_h, lay.obs_w, lay.obs_c) == (11, 11, 8)
+    assert lay.obs == 65536 * 4 * 11 * 11 * 8
+    assert lay.n_cand == 3464 and lay.jscratch == 0
+    assert lay.grid_stride == 400 and lay.ring_cap == 512
+    c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
+    assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
+    assert lay.obs_c == 32 and lay.obs == 8192 * 8 * 11 * 11 * 32
+    assert lay.n_cand == 16424 and lay.jscratch == 8192 * 16424 * 2
+    assert lay.grid == 8192 * 4 * 1600
+
+
+@pytest.mark.parametrize('kw,msg', [
+    (dict(num_snakes=0), 'num_snakes'), (dict(num_snakes=17), 'num_snakes'),
+    (dict(snake_length=1), 'snake_length'), (dict(height=2), 'height'),
+    (dict(num_fruits=0), 'num_fruits'), (dict(frame_stack=0), 'frame_stack'),
+    (dict(height=5, width=5, num_snakes=4, snake_length=3), 'too small'),
+])
+def test_plan_rejects(native, kw, msg):
+    c = cfg(native, **kw)
+    lay = native.SnakeLayout()
+    rc = native.lib().snake_plan(ctypes.byref(c), 16, ctypes.byref(lay))
+    assert rc == -1
+    assert msg in native.lib().snake_last_error().decode()
+    with pytest.raises(ValueError):
+        native.check(rc)
+
+
+def test_reward_dict_keys_are_checked(native):
+    from marlenv.config import build_cfg
+    with pytest.raises(KeyError):                   # snake_env.py:77-80
+        build_cfg(reward_dict={'fruit': 1.0})
+    c, meta = build_cfg(num_snakes=4)
+    assert meta['num_fruits'] == 3                  # int(round(0.8 * 4))
+    assert build_cfg(num_snakes=1)[1]['num_fruits'] == 1
+
+
+def table(native, H, W, L):
+    c = cfg(native, height=H, width=W, snake_length=L, num_snakes=1)
+    n = native.lib().snake_build_candidates(ctypes.byref(c), None, 0)
+    out = np.zeros(n * L, np.int16)
+    assert native.lib().snake_build_candidates(ctypes.byref(c), out.ctypes.data_as(ctypes.c_void_p), out.size) == n
+    cells = out.reshape(n, L).astype(np.int64)
+    return np.stack([cells // W, cells % W], -1).astype(np.int16)
+
+
+def test_spawn_table_matches_reference(native):
+    z = G.load('candidates.npz')
+    for k in z.files:
+        if k.startswith('full_'):
+            H, W = map(int, k.split('_')[1].split('x'))
+            L = int(k.split('_L')[1])
+            np.testing.assert_array_equal(table(native, H, W, L), z[k])
+    for H, W, L, C, dg in z['digest_meta']:
+        t = table(native, int(H), int(W), int(L))
+        assert t.shape[0] == int(C) and G.digest(t) == int(dg)

@@ -1,0 +1,275 @@
+"""Parity of the HIP path (through the C-ABI) with the reference: the golden
+fixtures generated from the real reference SnakeEnv, and the CPU oracle
+(oracle/snake_oracle.c, itself pinned to the fixtures) on seeded batches.
+Bar: bit-exact grids, dones, observations, info; float64 rewards compared by
+their bytes (identical, tolerance 0)."""
+import numpy as np
+import pytest
+
+import golden_io as G
+from parity_util import compare_step, oracle_batch
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('needs a HIP device')
+    from marlenv import _native
+    _native.lib()
+
+
+def _np(x):
+    return {k: v.cpu().numpy() for k, v in x.items()} if isinstance(x, dict) else x.cpu().numpy()
+
+
+# ------------------------------------------------------------- golden fixtures
+@pytest.mark.parametrize('name', G.traj_names())
+def test_compat_env_replays_golden(name):
+    """make_snake(num_envs=1)-style SnakeEnv following numpy's global RNG, exactly
+    as the reference does: np.random.seed(seed); env.reset(); env.step(...)."""
+    from marlenv.envs.snake_env import SnakeEnv
+    t = G.load_traj(name)
+    np.random.seed(t['seed'])
+    env = SnakeEnv(**G.env_kwargs(t['config']))
+    obs = env.reset()
+    np.testing.assert_array_equal(obs, t['obs0'])
+    n_reset = n_info = 0
+    full_at = {int(s): i for i, s in enumerate(t['full_obs_steps'])}
+    for i in range(len(t['actions'])):
+        obs, rews, dones, info = env.step([int(a) for a in t['actions'][i]])
+        assert isinstance(obs, np.ndarray) and obs.dtype == np.uint8
+        assert isinstance(rews, list) and isinstance(dones, list)
+        np.testing.assert_array_equal(env.grid, t['grids'][i], err_msg=f'{name} grid step {i}')
+        assert np.array(rews).tobytes() == t['rews'][i].tobytes(), (name, i, rews)
+        assert dones == t['dones'][i].tolist(), (name, i)
+        assert G.digest(obs) == int(t['obs_digest'][i]), (name, i)
+        if i in full_at:
+            np.testing.assert_array_equal(obs, t['full_obs'][full_at[i]])
+        assert env.alive_snakes == int(t['alive_snakes'][i])
+        if info:
+            assert int(t['info_step'][n_info]) == i
+            assert [int(x) for x in info['rank']] == t['info_rank'][n_info].tolist()
+            assert info['episode_scores'].tobytes() == t['info_scores'][n_info].tobytes()
+            assert info['episode_kills'].tobytes() == t['info_kills'][n_info].tobytes()
+            n_info += 1
+        else:
+            assert n_info >= len(t['info_step']) or int(t['info_step'][n_info]) != i
+        if t['reset_at'][i]:
+            n_reset += 1
+            o = env.reset()
+            np.testing.assert_array_equal(env.grid, t['reset_grid'][n_reset])
+            assert G.digest(o) == int(t['reset_obs_digest'][n_reset])
+    assert n_info == len(t['info_step'])
+
+
+@pytest.mark.parametrize('name', G.traj_names())
+def test_vec_env_autoreset_replays_golden(name):
+    """The batched env (N=1, per-env seed) with in-kernel auto-reset: the obs of
+    an all-done step is the reset observation (wrappers.py:139-145)."""
+    from marlenv import SnakeVecEnv
+    t = G.load_traj(name)
+    kw = G.env_kwargs(t['config'])
+    S = kw.pop('num_snakes')
+    v = SnakeVecEnv(1, num_snakes=S, seed=t['seed'], **kw)
+    assert G.digest(_np(v.reset())[0]) == int(t['obs0_digest'])
+    n_reset = 0
+    for i in range(len(t['actions'])):
+        obs, rew, done, info = v.step(torch.from_numpy(t['actions'][i][None].astype(np.int64)))
+        obs, rew, done = _np(obs)[0], _np(rew)[0], _np(done)[0]
+        assert rew.tobytes() == t['rews'][i].tobytes(), (name, i)
+        assert done.tolist() == t['dones'][i].tolist(), (name, i)
+        assert bool(info['episode_done'][0]) == bool(t['reset_at'][i])
+        if t['reset_at'][i]:
+            n_reset += 1
+            assert G.digest(obs) == int(t['reset_obs_digest'][n_reset]), (name, i)
+            np.testing.assert_array_equal(_np(v.grids())[0], t['reset_grid'][n_reset])
+        else:
+            assert G.digest(obs) == int(t['obs_digest'][i]), (name, i)
+            np.testing.assert_array_equal(_np(v.grids())[0], t['grids'][i])
+
+
+def test_crafted_scenarios():
+    from marlenv import SnakeVecEnv
+    for case in G.load_crafted():
+        kw = G.env_kwargs(case['config'])
+        S = kw.pop('num_snakes')
+        v = SnakeVecEnv(1, num_snakes=S, seed=case['seed'], autoreset=False, **kw)
+        v.inject(0, np.array(case['init_grid']), [(s['coords'], s['alive']) for s in case['snakes']],
+                 case['alive_snakes'], case['episode_length'])
+        for i, st in enumerate(case['steps']):
+            where = f"{case['name']} step {i}"
+            obs, rew, done, info = v.step(torch.tensor([st['actions']]))
+            np.testing.assert_array_equal(_np(v.grids())[0], np.array(st['grid']), err_msg=where)
+            assert _np(rew)[0].tobytes() == np.array(st['rews']).tobytes(), (where, _np(rew)[0], st['rews'])
+            assert _np(done)[0].tolist() == st['dones'], where
+            assert int(v.alive_counters()[0]) == st['alive_snakes'], where
+            np.testing.assert_array_equal(_np(obs)[0], st['obs'], err_msg=where)
+            tab = _np(v.snake_table())[0]
+            assert tab[:, 5].astype(bool).tolist() == st['alive'], where
+            live = [k for k in range(S) if st['alive'][k]]
+            assert tab[live, 0:2].tolist() == [st['heads'][k] for k in live], where
+            assert tab[live, 2:4].tolist() == [st['tails'][k] for k in live], where
+            assert tab[live, 6].tolist() == [st['lens'][k] for k in live], where
+            assert bool(info['episode_done'][0]) == bool(st['info']), where
+            if st['info']:
+                assert _np(info['rank'])[0].tolist() == st['info']['rank'], where
+                assert _np(info['episode_scores'])[0].tolist() == st['info']['episode_scores'], where
+
+
+# -------------------------------------------------------- batches vs the oracle
+BATCH_CASES = {
+    'cfg2_full20_s4': (dict(height=20, width=20, snake_length=3), 4, 96, 300),
+    'cfg3_vr5_s4': (dict(height=20, width=20, snake_length=3, vision_range=5), 4, 128, 300),
+    'cfg5_40_s8_vr5_fs4': (dict(height=40, width=40, snake_length=3, vision_range=5, frame_stack=4), 8, 24, 400),
+    'human_12_vr3_fs2': (dict(height=12, width=12, vision_range=3, frame_stack=2, observer='human'), 4, 64, 300),
+    'small_8_many_fruit': (dict(height=8, width=8, snake_length=2, num_fruits=20, vision_range=2), 3, 64, 300),
+    'l5_vr5': (dict(height=20, width=20, snake_length=5, vision_range=5), 4, 16, 150),
+    'kill_win_rewards': (dict(height=14, width=14, reward_dict={'fruit': 1.0, 'kill': 1.0, 'lose': -1.0,
+                                                               'win': 5.0, 'time': -0.01}), 4, 64, 300),
+    'single_s1': (dict(height=10, width=10, vision_range=4, num_fruits=4), 1, 64, 300),
+    'trunc_s2': (dict(height=12, width=12, max_episode_steps=7), 2, 64, 100),
+    's16': (dict(height=24, width=24, snake_length=2, vision_range=3), 16, 16, 200),
+}
+
+
+@pytest.mark.parametrize('case', sorted(BATCH_CASES))
+def test_batch_matches_oracle(oracle, case):
+    from marlenv import SnakeVecEnv
+    kw, S, N, T = BATCH_CASES[case]
+    seed = 1000 + 17 * len(case)
+    v = SnakeVecEnv(N, num_snakes=S, seed=seed, **kw)
+    obs0 = _np(v.reset())
+    refs, robs = oracle_batch(oracle, N, seed, S, **kw)
+    np.testing.assert_array_equal(obs0, robs)
+    rs = np.random.RandomState(seed)
+    n_act = 5 if kw.get('observer') == 'human' else 3
+    for t in range(T):
+        a = rs.randint(0, n_act, size=(N, S))
+        obs, rew, done, info = v.step(torch.from_numpy(a))
+        compare_step(refs, range(N), a, _np(obs), _np(rew), _np(done), _np(info),
+                     grids=_np(v.grids()), where=f'{case} step {t}')
+
+
+def test_coop_any_done(oracle):
+    """SnakeCoop-v1 (coop_snake_env.py:14-22): episode ends when any snake dies."""
+    from marlenv import SnakeVecEnv
+    N, S = 64, 4
+    v = SnakeVecEnv(N, num_snakes=S, seed=5, coop=True, autoreset=False, height=12, width=12)
+    v.reset()
+    rs = np.random.RandomState(3)
+    seen = 0
+    for t in range(40):
+        a = rs.randint(0, 3, size=(N, S))
+        _, _, done, info = v.step(torch.from_numpy(a))
+        d, ed = _np(done), _np(info['episode_done'])
+        assert (ed == d.any(1)).all()
+        assert (d[ed] == True).all()  # noqa: E712
+        seen += int(ed.sum())
+        if ed.any():
+            v.reset(torch.from_numpy(ed))
+    assert seen > 0
+
+
+def test_shards_equal_full_batch():
+    """Envs are keyed by global index: two shards == one batch (multi-GPU sharding)."""
+    from marlenv import SnakeVecEnv
+    N, S = 256, 4
+    kw = dict(height=20, width=20, vision_range=5)
+    full = SnakeVecEnv(N, num_snakes=S, seed=9, **kw)
+    parts = [SnakeVecEnv(N // 2, num_snakes=S, seed=9, env_offset=o, **kw) for o in (0, N // 2)]
+    o_full = full.reset()
+    o_parts = torch.cat([p.reset() for p in parts])
+    assert torch.equal(o_full, o_parts)
+    g = torch.Generator(device='cuda').manual_seed(1)
+    for t in range(150):
+        a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        of, rf, df, _ = full.step(a)
+        outs = [p.step(a[i * (N // 2):(i + 1) * (N // 2)]) for i, p in enumerate(parts)]
+        assert torch.equal(of, torch.cat([x[0] for x in outs]))
+        assert torch.equal(rf, torch.cat([x[1] for x in outs]))
+        assert torch.equal(df, torch.cat([x[2] for x in outs]))
+
+
+def test_full_size_sampled_parity(oracle):
+    """BASELINE config 3 at full size (65 536 envs): a sample of envs replayed
+    through the oracle bit-exactly, plus whole-batch invariants."""
+    from marlenv import SnakeVecEnv
+    N, S, T = 65536, 4, 120
+    kw = dict(height=20, width=20, snake_length=3, vision_range=5)
+    v = SnakeVecEnv(N, num_snakes=S, seed=0, **kw)
+    obs = v.reset()
+    idx = np.unique(np.concatenate([np.arange(8), np.linspace(0, N - 1, 40).astype(int),
+                                    np.random.RandomState(0).randint(0, N, 16)]))
+    refs = {int(i): oracle.OracleEnv(seed=int(i), num_snakes=S, **kw) for i in idx}
+    o0 = obs[torch.from_numpy(idx).cuda()].cpu().numpy()
+    for row, i in enumerate(idx):
+        assert (refs[int(i)].reset() == o0[row]).all()
+    g = torch.Generator(device='cuda').manual_seed(12345)
+    n_ep = 0
+    sel = torch.from_numpy(idx).cuda()
+    for t in range(T):
+        a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        obs, rew, done, info = v.step(a)
+        n_ep += int(info['episode_done'].sum())
+        sub = {k: x[sel].cpu().numpy() for k, x in info.items()}
+        compare_step([refs[int(i)] for i in idx], range(len(idx)), a[sel].cpu().numpy(),
+                     obs[sel].cpu().numpy(), rew[sel].cpu().numpy(), done[sel].cpu().numpy(), sub,
+                     where=f'full-size step {t}')
+        # invariants over every env: one own-head cell at the crop centre of each
+        # alive snake; no own-head channel for dead snakes
+        tab = v.snake_table()
+        alive = tab[..., 5].bool()
+        centre = obs[:, :, 5, 5, 5]
+        heads = obs[..., 5].sum(dim=(2, 3))
+        assert torch.equal(centre.bool() | ~alive, torch.ones_like(alive))
+        assert torch.equal(heads[alive], torch.ones_like(heads[alive]))
+        assert int(heads[~alive].sum()) == 0
+        assert not bool(info['error'].any())
+    assert n_ep > 0.005 * N * T / 60
+
+
+def test_invalid_actions():
+    from marlenv import SnakeVecEnv
+    from marlenv.envs.snake_env import SnakeEnv
+    env = SnakeEnv(num_snakes=2)
+    env.reset()
+    g = env.grid
+    with pytest.raises(KeyError):
+        env.step([0, 3])
+    np.testing.assert_array_equal(env.grid, g)   # env untouched
+    env.step([0, 0])
+    v = SnakeVecEnv(4, num_snakes=2, seed=1)
+    v.reset()
+    _, _, _, info = v.step(torch.tensor([[0, 0], [0, 7], [1, 2], [-1, 0]]))
+    assert _np(info['error']).tolist() == [0, 1, 0, 1]
+    vs = SnakeVecEnv(2, num_snakes=2, seed=1, strict=True)
+    vs.reset()
+    with pytest.raises(KeyError):
+        vs.step(torch.tensor([[0, 0], [0, 5]]))
+
+
+def test_make_snake_surface():
+    from marlenv import make_snake
+    env, a, b, props = make_snake(num_envs=1, num_snakes=4, height=20, width=20, vision_range=5)
+    assert a is None and b is None
+    assert props == {'action_info': {'action_n': 3}, 'num_envs': 1, 'num_snakes': 4}
+    assert env.observation_space.shape == (4, 11, 11, 8)
+    assert env.action_space.n == 3
+    obs = env.reset()
+    assert obs.shape == (4, 11, 11, 8) and obs.dtype == np.uint8
+    acts = [env.action_space.sample() for _ in range(4)]
+    obs2, rews, dones, info = env.step(acts)
+    assert len(rews) == 4 and all(isinstance(r, float) for r in rews)
+    assert obs2 is not obs
+    single, _, _, p1 = make_snake(num_envs=1, num_snakes=1)
+    o = single.reset()
+    assert o.shape == (20, 20, 8)
+    o, r, d, i = single.step(0)
+    assert isinstance(r, float) and isinstance(d, bool) and i == {}
+    venv, _, _, pv = make_snake(num_envs=64, num_snakes=4, vision_range=5)
+    assert pv['num_envs'] == 64
+    ob = venv.reset()
+    assert tuple(ob.shape) == (64, 4, 11, 11, 8) and ob.is_cuda

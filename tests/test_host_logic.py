@@ -1,0 +1,45 @@
+"""Host-side logic that needs no GPU: env-id registry, wrappers' spaces,
+sharding arithmetic used by bench.py, and the library refusing to run
+without a HIP device (no CPU fallback)."""
+import numpy as np
+import pytest
+
+
+def test_graph_env_is_out_of_scope():
+    from marlenv import make_snake
+    with pytest.raises(NotImplementedError):
+        make_snake(num_envs=1, env_id='SnakeGraph-v1')
+    with pytest.raises(KeyError):
+        make_snake(num_envs=1, env_id='Nope-v0')
+
+
+def test_no_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from marlenv import SnakeVecEnv
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        SnakeVecEnv(4, num_snakes=4)
+
+
+def test_spaces():
+    from marlenv import spaces
+    d = spaces.Discrete(3, seed=0)
+    xs = {d.sample() for _ in range(200)}
+    assert xs == {0, 1, 2}
+    st = np.random.get_state()
+    d.sample()
+    assert (np.random.get_state()[1] == st[1]).all()   # never touches the global RNG
+    b = spaces.Box(0, 255, (4, 11, 11, 8), np.uint8)
+    assert b.shape == (4, 11, 11, 8) and b.contains(np.zeros(b.shape, np.uint8))
+
+
+def test_shard_ranges():
+    from bench import shard_range
+    N = 262144
+    for G in (1, 2, 4, 8):
+        spans = [shard_range(N, G, r) for r in range(G)]
+        assert spans[0][0] == 0 and spans[-1][1] == N
+        for (a, b), (c, d) in zip(spans, spans[1:]):
+            assert b == c
+        assert sum(b - a for a, b in spans) == N
