@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 1
+#define SNAKE_ABI_VERSION 2
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -58,6 +58,7 @@ typedef struct {
     int64_t snake;      /* int32  [N][S][4]              packed snake records */
     int64_t body;       /* uint8  [N][S][ring_cap]       direction deques (rings) */
     int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos */
+    int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */
     int64_t stats;      /* double [N][4][S]              episode scores/steps/fruits/kills */
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
     int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
@@ -79,6 +80,7 @@ typedef struct {        /* device state buffers (layouts in snake_layout) */
     int32_t  *snake;
     uint8_t  *body;
     int32_t  *env;
+    uint16_t *ctr;
     double   *stats;
     uint32_t *mt;
     const int16_t *cand;

@@ -192,6 +192,7 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->snake = N * S * 4 * 4;
     o->body = N * S * o->ring_cap;
     o->env = N * kEnvRec * 4;
+    o->ctr = N * fs * S * 2;
     o->stats = N * 4 * S * 8;
     o->mt = N * kMtN * 4;
     o->cand = o->n_cand * c->snake_length * 2;
@@ -256,8 +257,8 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
 
 static int check_state(const KCfg &k, const snake_state *st, bool need_all)
 {
-    if (!st || !st->grid || !st->snake || !st->body || !st->env || !st->stats || !st->mt ||
-        !st->cand) {
+    if (!st || !st->grid || !st->snake || !st->body || !st->env || !st->ctr || !st->stats ||
+        !st->mt || !st->cand) {
         set_error("snake_state has a NULL buffer");
         return SNAKE_E_ARG;
     }

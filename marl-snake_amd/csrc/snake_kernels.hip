@@ -1,15 +1,17 @@
 // snake_kernels.hip -- the batched multi-snake env step on CDNA4 (gfx950).
 //
 // One 64-lane wavefront (= one workgroup) per env instance:
-//   * the env's grid ring (fs int8 H x W frames) is staged in LDS with 16-byte loads;
-//   * the order-dependent game rules (snake_env.py:301-374) run as wave-uniform
-//     scalar code over a handful of snakes;
+//   * the env's grid ring (fs uint8 H x W frames) is staged in LDS with 16-byte loads;
+//   * the game rules (snake_env.py:301-374) run lane-parallel, lane k = snake k:
+//     targets, collision groups (readlane broadcasts), the fruit-eater tail
+//     rule, rewards, and a two-phase grid update (all tail clears, then all
+//     BODY/HEAD/TAIL writes) that reproduces the reference's snake-order update
+//     exactly ("two-phase update");
 //   * the wave-parallel parts use all 64 lanes: dead-body erase (prefix-scanned
 //     direction deque), fruit respawn (lane-chunked empty-cell ranking + MT19937
-//     rejection sampling resolved by ballots), episode statistics (lane = snake),
-//     the NHWC one-hot observation encode (16-byte coalesced stores), and the
-//     auto-reset (in-register MT19937 twist, ballot-resolved Fisher-Yates draws,
-//     backward permutation trace).
+//     rejection sampling resolved by ballots), the NHWC one-hot observation
+//     encode (16-byte coalesced stores), and the auto-reset (in-register MT19937
+//     twist, ballot-resolved Fisher-Yates draws, backward permutation trace).
 // Compiled with -ffp-contract=off: rewards/statistics are float64 in the
 // reference's order of operations (snake_env.py:365-369, :385-389).
 #include <hip/hip_runtime.h>
@@ -23,6 +25,16 @@ enum { C_EMPTY = 0, C_WALL = 1, C_FRUIT = 2, C_HEAD = 3, C_BODY = 4, C_TAIL = 5 
 // Direction (core/snake.py:33-37): 0 UP(-1,0) 1 RIGHT(0,1) 2 DOWN(1,0) 3 LEFT(0,-1)
 __device__ __forceinline__ int dir_dr(int d) { return d == 0 ? -1 : (d == 2 ? 1 : 0); }
 __device__ __forceinline__ int dir_dc(int d) { return d == 1 ? 1 : (d == 3 ? -1 : 0); }
+__device__ __forceinline__ int div10(int v) { return (v * 205) >> 11; }  // exact for 0 <= v < 1029
+
+// LDS hand-off between lanes of the single wave of a workgroup: LDS executes a
+// wave's instructions in order, so only the compiler must not move memory
+// operations across this point.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 
 __device__ __forceinline__ int wave_scan(int v, int lane)
 {
@@ -34,27 +46,7 @@ __device__ __forceinline__ int wave_scan(int v, int lane)
     return v;
 }
 
-// a[k] for a wave-uniform runtime k over a register array. Written as masked ORs
-// (not selects): InstCombine folds a select of two loads into a load through a
-// selected pointer, which would keep the whole array in scratch.
-template <int MS>
-__device__ __forceinline__ int pick(const int (&a)[MS], int k)
-{
-    int v = 0;
-#pragma unroll
-    for (int i = 0; i < MS; i++) v |= a[i] & -(int)(k == i);
-    return v;
-}
-
-template <int MS>
-__device__ __forceinline__ double pick(const double (&a)[MS], int k)
-{
-    unsigned long long v = 0;
-#pragma unroll
-    for (int i = 0; i < MS; i++)
-        v |= (unsigned long long)__double_as_longlong(a[i]) & (0ull - (unsigned long long)(k == i));
-    return __longlong_as_double((long long)v);
-}
+__device__ __forceinline__ int bcast(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
 __device__ __forceinline__ uint32_t gen_mask(uint32_t m)
 {
@@ -79,6 +71,9 @@ __device__ __forceinline__ uint32_t temper(uint32_t y)
     return y;
 }
 
+// m.w[t] for a wave-uniform runtime t. Masked ORs, not selects: InstCombine turns
+// a select of two loads into a load through a selected pointer, which would
+// demote the whole register array to scratch.
 __device__ __forceinline__ uint32_t word_at(const WaveMT &m, int t)
 {
     uint32_t v = 0;
@@ -108,7 +103,7 @@ __device__ __forceinline__ void mt_store(const WaveMT &m, uint32_t *g, int lane)
 
 // mt19937_gen, wave-parallel. new[i] = X ^ (y >> 1) ^ mag(y), y = old[i]|old[i+1]
 // (upper/lower bits), X = old[i+397] for i < 227 and new[i-227] after; the last
-// word mixes new[0]. Every element's inputs sit in a fixed lane offset (13 for
+// word mixes new[0]. Every element's inputs sit at a fixed lane offset (13 for
 // i+397, 29 for i-227) of an earlier register, so the twist is 10 register steps.
 __device__ void mt_twist(WaveMT &m, int lane)
 {
@@ -120,9 +115,8 @@ __device__ void mt_twist(WaveMT &m, int lane)
         const int e = 64 * t + lane;
         const uint32_t cur = m.w[t];
         const uint32_t same = __shfl(cur, l1);
-        const uint32_t nxt = __shfl(m.w[t < 9 ? t + 1 : 9], 0);
+        const uint32_t nxt = __builtin_amdgcn_readlane(m.w[t < 9 ? t + 1 : 9], 0);
         uint32_t o1 = (lane == 63) ? nxt : same;
-        uint32_t x = 0;
         uint32_t xold = 0, xnew = 0;
         if (t <= 3) {
             const uint32_t a = __shfl(m.w[t + 6 <= 9 ? t + 6 : 9], l13);
@@ -134,10 +128,10 @@ __device__ void mt_twist(WaveMT &m, int lane)
             const uint32_t b = __shfl(nw[t - 3 >= 0 ? t - 3 : 0], l29);
             xnew = (lane + 29 < 64) ? a : b;
         }
-        x = (e < 227) ? xold : xnew;
+        uint32_t x = (e < 227) ? xold : xnew;
         if (t == 9) {
-            const uint32_t n0 = __shfl(nw[0], 0);
-            const uint32_t n396 = __shfl(nw[6], 12);
+            const uint32_t n0 = __builtin_amdgcn_readlane(nw[0], 0);
+            const uint32_t n396 = __builtin_amdgcn_readlane(nw[6], 12);
             if (e == kMtN - 1) { o1 = n0; x = n396; }
         }
         const uint32_t y = (cur & UPPER) | (o1 & LOWER);
@@ -162,31 +156,34 @@ __device__ uint32_t mt_draw(WaveMT &m, uint32_t mask, uint32_t rng, int lane)
         if (b) {
             const int f = __ffsll((long long)b) - 1;
             m.pos = (t << 6) + f + 1;
-            return __shfl(v, f);
+            return (uint32_t)bcast((int)v, f);
         }
         m.pos = min((t + 1) << 6, kMtN);
     }
 }
 
 // permutation(n) = shuffle(arange(n)) draws j_i = random_interval(i) for
-// i = n-1 .. 1 (snake_env.py:581). Writes jarr[i] = j_i. A round tempers 64 raw
-// words; lane l (offset d from the first unread word) is a SURE reject when
-// w > i, a SURE accept when w <= i - d (at most d accepts precede it), else
-// ambiguous: everything before the first ambiguous lane is resolved at once
-// with ballots, the ambiguous lane with the exact accept count. Rounds never
-// straddle a change of mask (i crossing a power of two).
+// i = n-1 .. 1 (snake_env.py:581). Writes jarr[i] = j_i. A round covers the 64
+// raw words of one tempered register; lane l (offset d from the first unread
+// word) is a SURE reject when w > i, a SURE accept when w <= i - d (at most d
+// accepts precede it), else ambiguous: everything before the first ambiguous
+// lane is resolved at once with ballots, the ambiguous lane with the exact
+// accept count. Rounds never straddle a change of mask (i crossing 2^k).
 __device__ void mt_perm_draws(WaveMT &m, int n, uint16_t *jarr, int lane)
 {
     int i = n - 1;
+    int tc = -1;
+    uint32_t tw = 0;
     while (i >= 1) {
-        if (m.pos >= kMtN) mt_twist(m, lane);
+        if (m.pos >= kMtN) { mt_twist(m, lane); tc = -1; }
+        const int t = m.pos >> 6, l0 = m.pos & 63;
+        if (t != tc) { tw = temper(word_at(m, t)); tc = t; }
         const uint32_t mask = gen_mask((uint32_t)i);
         const int lo = (int)(mask >> 1) + 1;
-        const int t = m.pos >> 6, l0 = m.pos & 63;
         const int e = (t << 6) + lane;
         const int lim = l0 + (i - lo);
         const bool valid = lane >= l0 && lane <= lim && e < kMtN;
-        const uint32_t w = temper(word_at(m, t)) & mask;
+        const uint32_t w = tw & mask;
         const int d = lane - l0;
         const bool rej = w > (uint32_t)i;
         const bool sure = !rej && (int)w <= i - d;
@@ -203,7 +200,7 @@ __device__ void mt_perm_draws(WaveMT &m, int n, uint16_t *jarr, int lane)
         }
         int A = __popcll(acc);
         if (am) {
-            const uint32_t wf = __shfl(w, end);
+            const uint32_t wf = (uint32_t)bcast((int)w, end);
             if ((int)wf <= i - A) {
                 if (lane == 0) jarr[i - A] = (uint16_t)wf;
                 A++;
@@ -217,7 +214,9 @@ __device__ void mt_perm_draws(WaveMT &m, int n, uint16_t *jarr, int lane)
 }
 
 // Final arr[k] of the Fisher-Yates pass for k < S: walk each position
-// backwards through the swaps (i ascending = reverse of the draw order).
+// backwards through the swaps (i ascending = reverse of the draw order). A
+// chunk of 64 swaps that touches none of the S tracked positions costs one
+// ballot.
 template <int MS>
 __device__ void perm_trace(int n, const uint16_t *jarr, int S, int (&q)[MS], int lane)
 {
@@ -226,6 +225,10 @@ __device__ void perm_trace(int n, const uint16_t *jarr, int S, int (&q)[MS], int
     for (int b = 1; b < n; b += kWave) {
         const int i = b + lane;
         const int jv = (i < n) ? (int)jarr[i] : -1;
+        bool hit = false;
+#pragma unroll
+        for (int k = 0; k < MS; k++) hit |= (k < S) && (i == q[k] || jv == q[k]);
+        if (__ballot(hit && i < n) == 0ull) continue;
 #pragma unroll
         for (int k = 0; k < MS; k++) {
             if (k >= S) continue;
@@ -235,7 +238,7 @@ __device__ void perm_trace(int n, const uint16_t *jarr, int S, int (&q)[MS], int
                     __ballot(i < n && lane > from && (i == q[k] || jv == q[k]));
                 if (!mk) break;
                 const int f = __ffsll((long long)mk) - 1;
-                const int jf = __shfl(jv, f);
+                const int jf = bcast(jv, f);
                 q[k] = (b + f == q[k]) ? jf : b + f;
                 from = f;
             }
@@ -253,7 +256,7 @@ __device__ void place_fruits(const KCfg &c, uint8_t *g, WaveMT &m, int k, uint16
     int cnt = 0;
     for (int x = c0; x < c1; x++) cnt += (g[x] == C_EMPTY);
     const int incl = wave_scan(cnt, lane), excl = incl - cnt;
-    const int E = __shfl(incl, 63);
+    const int E = bcast(incl, 63);
     if (E == 0) return;  // no empty cell: no draw (random_empty_coords returns None)
     const uint32_t rng = (uint32_t)(E - 1), mask = gen_mask(rng);
     for (int d = 0; d < k; d++) {
@@ -268,57 +271,31 @@ __device__ void place_fruits(const KCfg &c, uint8_t *g, WaveMT &m, int k, uint16
             }
         }
     }
-    __syncthreads();
+    wave_sync();
     for (int d = lane; d < k; d += kWave) g[fbuf[d]] = C_FRUIT;
-    __syncthreads();
+    wave_sync();
 }
 
 // ------------------------------------------------------------------ encode
-// _encode (snake_env.py:474-519) + frame stack (:444-472): for snake k the
-// 8 channels [wall, fruit, other head/body/tail, own head/body/tail]; with a
-// vision range the (2vr+1)^2 window is centred on the first own-HEAD cell in
-// row-major order ((0,0) when the snake is dead) and zero outside the grid.
-__device__ void find_centers(const KCfg &c, const uint8_t *frame, int *ctr, int lane)
-{
-    if (lane < kMaxSnakes) ctr[lane] = 0x7fffffff;
-    __syncthreads();
-    const int c0 = lane * c.cs, c1 = min(c.HW, c0 + c.cs);
-    for (int x = c0; x < c1; x++) {
-        const int v = frame[x];
-        if (v >= 3 && v % 10 == C_HEAD) {
-            const int id = (v * 205) >> 11;  // v / 10 for v < 1029
-            if (id < c.S) atomicMin(&ctr[id], x);
-        }
-    }
-    __syncthreads();
-    if (lane < kMaxSnakes) {
-        int x = ctr[lane];
-        if (x == 0x7fffffff) x = 0;
-        ctr[lane] = ((x / c.W) << 16) | (x % c.W);
-    }
-    __syncthreads();
-}
-
+// _encode (snake_env.py:474-519) + frame stack (:444-472): for snake k the 8
+// channels [wall, fruit, other head/body/tail, own head/body/tail]; with a vision
+// range the (2vr+1)^2 window is centred on the own-HEAD cell (argmax of the own
+// head plane: the snake's head while alive, (0,0) once dead) and zero outside
+// the grid. org[f*16+k] = crop origin of snake k in frame f, packed
+// ((r0 + 256) << 16) | (c0 + 256).
 __device__ __forceinline__ unsigned long long onehot(int v, int k)
 {
-    if (v == C_EMPTY) return 0ull;
-    if (v == C_WALL) return 1ull;
-    if (v == C_FRUIT) return 1ull << 8;
-    const int id = (v * 205) >> 11;
-    const int code = v - 10 * id;                 // 3 HEAD, 4 BODY, 5 TAIL
-    const int ch = (id == k) ? code + 2 : code - 1;
-    return 1ull << (8 * ch);
+    const int id = div10(v);
+    const int code = v - 10 * id;                   // 3 HEAD, 4 BODY, 5 TAIL
+    const int ch = (v < 3) ? v - 1 : ((id == k) ? code + 2 : code - 1);
+    return v == C_EMPTY ? 0ull : (1ull << (8 * ch));
 }
 
 __device__ __forceinline__ unsigned long long unit_bits(const KCfg &c, const uint8_t *frames,
-                                                       const int *ctr, int k, int i, int j, int f)
+                                                       const int *org, int k, int i, int j, int f)
 {
-    int r = i, cc = j;
-    if (c.vr) {
-        const int p = ctr[f * kMaxSnakes + k];
-        r = (p >> 16) - c.vr + i;
-        cc = (p & 0xffff) - c.vr + j;
-    }
+    const int p = org[f * kMaxSnakes + k];
+    const int r = (p >> 16) - 256 + i, cc = (p & 0xffff) - 256 + j;
     if ((unsigned)r >= (unsigned)c.H || (unsigned)cc >= (unsigned)c.W) return 0ull;
     return onehot(frames[f * c.grid_stride + r * c.W + cc], k);
 }
@@ -326,7 +303,7 @@ __device__ __forceinline__ unsigned long long unit_bits(const KCfg &c, const uin
 // obs layout (S, oh, ow, 8*fs): unit u = ((k*oh + i)*ow + j)*fs + f is 8 bytes.
 // Lane l writes units 2l, 2l+1 (16 bytes) then strides by 128 units; the
 // (k,i,j,f) digits advance by carries, no division in the loop.
-__device__ void encode(const KCfg &c, const uint8_t *frames, const int *ctr, uint8_t *obs_env, int lane)
+__device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, uint8_t *obs_env, int lane)
 {
     const int U = c.units, pairs = (U + 1) >> 1;
     int u = 2 * lane;
@@ -337,14 +314,14 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *ctr, uin
     int k = rest / c.oh;
     const bool wide = (U & 1) == 0;
     for (int p = lane; p < pairs; p += kWave) {
-        const unsigned long long a = unit_bits(c, frames, ctr, k, i, j, f);
+        const unsigned long long a = unit_bits(c, frames, org, k, i, j, f);
         int f2 = f + 1, j2 = j, i2 = i, k2 = k;
         if (f2 == c.fs) {
             f2 = 0;
             if (++j2 == c.ow) { j2 = 0; if (++i2 == c.oh) { i2 = 0; k2++; } }
         }
         const bool has_b = 2 * p + 1 < U;
-        const unsigned long long b = has_b ? unit_bits(c, frames, ctr, k2, i2, j2, f2) : 0ull;
+        const unsigned long long b = has_b ? unit_bits(c, frames, org, k2, i2, j2, f2) : 0ull;
         if (wide) {
             uint4 v;
             v.x = (uint32_t)a; v.y = (uint32_t)(a >> 32);
@@ -364,10 +341,9 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *ctr, uin
     }
 }
 
-__device__ __forceinline__ void copy_lds_to_global(uint8_t *dst, const uint8_t *src, int bytes, int lane)
+__device__ __forceinline__ int pack_origin(const KCfg &c, int r, int cc)
 {
-    for (int q = lane; q < (bytes >> 4); q += kWave)
-        reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(src)[q];
+    return c.vr ? (((r - c.vr + 256) << 16) | (cc - c.vr + 256)) : ((256 << 16) | 256);
 }
 
 __device__ __forceinline__ int dir_of_diff(int diff, int W)
@@ -385,7 +361,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
                          WaveMT &mt, uint8_t *lds, int lane)
 {
     uint8_t *frames = lds + c.lds_frames;
-    int *ctr = reinterpret_cast<int *>(lds + c.lds_centers);
+    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
     uint16_t *jarr = c.jarr_in_lds ? reinterpret_cast<uint16_t *>(lds + c.lds_jarr)
                                    : st.jscratch + (int64_t)e * c.n_cand;
@@ -397,17 +373,19 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     // poses would hang the wave, so give up after 2^16 permutations.
     for (int attempt = 0; attempt < (1 << 16); attempt++) {
         mt_perm_draws(mt, c.n_cand, jarr, lane);
-        __syncthreads();
+        if (c.jarr_in_lds) wave_sync(); else __syncthreads();
         int q[MS];
         perm_trace<MS>(c.n_cand, jarr, S, q, lane);
-        const int pk = pick<MS>(q, sk < MS ? sk : 0);
+        int pk = 0;
+#pragma unroll
+        for (int k = 0; k < MS; k++) pk = (sk == k) ? q[k] : pk;
         cell = (lane < SL) ? (int)st.cand[(int64_t)pk * L + si] : -1;
         bool dup = false;
         for (int x = 0; x < SL; x++) {
-            const int cx = __shfl(cell, x);
+            const int cx = bcast(cell, x);
             dup |= (lane < SL && lane != x && cx == cell);
         }
-        __syncthreads();
+        if (c.jarr_in_lds) wave_sync(); else __syncthreads();
         if (__ballot(dup) == 0ull) break;   // _clear_overlap (:568-574)
     }
     // make_grid (grid_util.py:14-20), then paint (:138-144)
@@ -415,7 +393,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         const int r = x / W, cc = x - r * W;
         work[x] = (r == 0 || cc == 0 || r == c.H - 1 || cc == W - 1) ? C_WALL : C_EMPTY;
     }
-    __syncthreads();
+    wave_sync();
     const int nxt = __shfl(cell, (lane + 1) & 63);
     const int tailcell = __shfl(cell, min(lane + L - 1, 63));
     if (lane < SL) {
@@ -431,32 +409,31 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
             rec.z = 0 | ((L - 1) << 16);
             rec.w = 0;
             reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + sk] = rec;
+            const int og = pack_origin(c, hr, hc);
+            for (int f = 0; f < c.fs; f++) {
+                org[f * kMaxSnakes + sk] = og;
+                st.ctr[((int64_t)e * c.fs + f) * S + sk] = (uint16_t)((hr << 8) | hc);
+            }
         }
     }
-    __syncthreads();
+    wave_sync();
     place_fruits(c, work, mt, c.num_fruits, fbuf, lane);        // :147-148
     uint8_t *gbase = st.grid + (int64_t)e * c.fs * c.grid_stride;
-    for (int s = 0; s < c.fs; s++) copy_lds_to_global(gbase + s * c.grid_stride, work, c.grid_stride, lane);
-    for (int s = 0; s < c.fs - 1; s++)
-        for (int q = lane; q < (c.grid_stride >> 4); q += kWave)
-            reinterpret_cast<uint4 *>(frames + s * c.grid_stride)[q] = reinterpret_cast<const uint4 *>(work)[q];
+    const int n16 = c.grid_stride >> 4;
+    for (int q = lane; q < n16; q += kWave) {
+        const uint4 v = reinterpret_cast<const uint4 *>(work)[q];
+        for (int s = 0; s < c.fs; s++) reinterpret_cast<uint4 *>(gbase + s * c.grid_stride)[q] = v;
+        for (int s = 0; s < c.fs - 1; s++) reinterpret_cast<uint4 *>(frames + s * c.grid_stride)[q] = v;
+    }
     if (lane == 0) {
-        int32_t *er = st.env + (int64_t)e * kEnvRec;
-        er[ENV_ALIVE] = S;
-        er[ENV_EPLEN] = 0;
-        er[ENV_CUR] = c.fs - 1;
-        er[ENV_MTPOS] = mt.pos;
+        int4 er;
+        er.x = S; er.y = 0; er.z = c.fs - 1; er.w = mt.pos;
+        *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = er;
     }
     if (lane < 4 * S) st.stats[(int64_t)e * 4 * S + lane] = 0.0;   // _reset_epi_stats
     mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
-    __syncthreads();
-    if (c.vr) {
-        find_centers(c, work, ctr + (c.fs - 1) * kMaxSnakes, lane);
-        for (int x = lane; x < (c.fs - 1) * kMaxSnakes; x += kWave)
-            ctr[x] = ctr[(c.fs - 1) * kMaxSnakes + (x & (kMaxSnakes - 1))];
-        __syncthreads();
-    }
-    encode(c, frames, ctr, o.obs + (int64_t)e * c.units * 8, lane);
+    wave_sync();
+    encode(c, frames, org, o.obs + (int64_t)e * c.units * 8, lane);
 }
 
 // -------------------------------------------------------------------- step
@@ -466,186 +443,161 @@ __global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int e = blockIdx.x, lane = threadIdx.x;
-    const int S = c.S, W = c.W, cap = c.ring_cap;
+    const int S = c.S, W = c.W, cap = c.ring_cap, fs = c.fs;
     uint8_t *frames = lds + c.lds_frames;
-    int *ctr = reinterpret_cast<int *>(lds + c.lds_centers);
+    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
-    uint8_t *work = frames + (c.fs - 1) * c.grid_stride;
-    int32_t *er = st.env + (int64_t)e * kEnvRec;
-    const int alive0 = er[ENV_ALIVE], eplen = er[ENV_EPLEN], cur = er[ENV_CUR], mtpos = er[ENV_MTPOS];
+    uint8_t *work = frames + (fs - 1) * c.grid_stride;
+    const int4 er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
+    const int alive0 = er.x, eplen = er.y, cur = er.z, mtpos = er.w;
+    const bool isn = lane < S;
 
+    // snake k's record in lane k: head/tail coords, heading, alive, deque ring
+    int4 rec = make_int4(0, 0, 0, 0);
+    int act = 0;
+    if (isn) {
+        rec = reinterpret_cast<const int4 *>(st.snake)[(int64_t)e * S + lane];
+        act = actions[(int64_t)e * S + lane];
+    }
     // Stage the grid ring: LDS frame x < fs-1 <- slot (cur+2+x) % fs (the fs-1
     // most recent frames, oldest first); LDS frame fs-1 (work) <- slot cur.
-    const uint8_t *gbase = st.grid + (int64_t)e * c.fs * c.grid_stride;
+    const uint8_t *gbase = st.grid + (int64_t)e * fs * c.grid_stride;
     const int n16 = c.grid_stride >> 4;
-    for (int x = 0; x < c.fs; x++) {
-        const int slot = (x == c.fs - 1) ? cur : (cur + 2 + x) % c.fs;
+    for (int x = 0; x < fs; x++) {
+        const int slot = (x == fs - 1) ? cur : (cur + 2 + x) % fs;
         for (int q = lane; q < n16; q += kWave)
             reinterpret_cast<uint4 *>(frames + x * c.grid_stride)[q] =
                 reinterpret_cast<const uint4 *>(gbase + slot * c.grid_stride)[q];
     }
-
-    // Snake records (wave-uniform): head/tail coords, heading, alive, deque ring.
-    int hr[MS], hc[MS], tr[MS], tc[MS], dir[MS], alive[MS], rh[MS], rl[MS], tdir[MS], act[MS];
-    const uint8_t *ring0 = st.body + (int64_t)e * S * cap;
-#pragma unroll
-    for (int k = 0; k < MS; k++) {
-        hr[k] = hc[k] = tr[k] = tc[k] = dir[k] = alive[k] = rh[k] = rl[k] = tdir[k] = act[k] = 0;
-        if (k < S) {
-            const int4 r = reinterpret_cast<const int4 *>(st.snake)[(int64_t)e * S + k];
-            hr[k] = r.x & 255; hc[k] = (r.x >> 8) & 255; tr[k] = (r.x >> 16) & 255; tc[k] = (r.x >> 24) & 255;
-            dir[k] = r.y & 3; alive[k] = (r.y >> 8) & 1;
-            rh[k] = r.z & 0xffff; rl[k] = (r.z >> 16) & 0xffff;
-            act[k] = actions[(int64_t)e * S + k];
-            // the tail direction move() pops (core/snake.py:103): prefetched
-            if (alive[k]) tdir[k] = ring0[(int64_t)k * cap + ((rh[k] + rl[k] - 1) & (cap - 1))];
-        }
+    if (fs > 1 && lane < (fs - 1) * S) {      // crop origins of the kept older frames
+        const int x = lane / S, k = lane - x * S;
+        const int slot = (cur + 2 + x) % fs;
+        const int p = st.ctr[((int64_t)e * fs + slot) * S + k];
+        org[x * kMaxSnakes + k] = pack_origin(c, p >> 8, p & 255);
     }
+    int hr = rec.x & 255, hc = (rec.x >> 8) & 255, tr = (rec.x >> 16) & 255, tc = (rec.x >> 24) & 255;
+    int dir = rec.y & 3, alive = (rec.y >> 8) & 1;
+    int rh = rec.z & 0xffff, rl = (rec.z >> 16) & 0xffff;
+    uint8_t *ring = st.body + ((int64_t)e * S + lane) * cap;
+    // the tail direction move() pops (core/snake.py:103), prefetched
+    const int tdir = (isn && alive) ? ring[(rh + rl - 1) & (cap - 1)] : 0;
 
     // snake_env.py:318-330 heading + target cell per alive snake
-    int mv[MS], ncell[MS];
-    bool bad = false;
-#pragma unroll
-    for (int k = 0; k < MS; k++) {
-        mv[k] = 0; ncell[k] = -1;
-        if (k < S && alive[k]) {
-            const int a = act[k], d = dir[k];
-            int nd = d;
-            if (c.observer == 0) {          // _next_direction :598-608 (0 keep, 1 left, 2 right)
-                if (a < 0 || a > 2) bad = true;
-                nd = (a == 1) ? ((d + 3) & 3) : ((a == 2) ? ((d + 1) & 3) : d);
-            } else if (dir_dr(d) == 0) {    // _next_direction_global :610-632
-                if (a == 3) nd = 2; else if (a == 4) nd = 0;
-            } else {
-                if (a == 1) nd = 3; else if (a == 2) nd = 1;
-            }
-            dir[k] = nd;
-            ncell[k] = (hr[k] + dir_dr(nd)) * W + hc[k] + dir_dc(nd);
-            mv[k] = 1;
-        }
+    const bool mv = isn && alive;
+    int nd = dir;
+    if (c.observer == 0) {                 // _next_direction :598-608 (0 keep, 1 left, 2 right)
+        nd = (act == 1) ? ((dir + 3) & 3) : ((act == 2) ? ((dir + 1) & 3) : dir);
+    } else if (dir_dr(dir) == 0) {         // _next_direction_global :610-632
+        nd = (act == 3) ? 2 : ((act == 4) ? 0 : dir);
+    } else {
+        nd = (act == 1) ? 3 : ((act == 2) ? 1 : dir);
     }
-    if (bad) {                 // action_angle_dict[action] raises KeyError: env untouched
-        if (lane == 0) o.err[e] = 1;
+    if (__ballot(mv && c.observer == 0 && (act < 0 || act > 2))) {
+        if (lane == 0) o.err[e] = 1;       // action_angle_dict[action] KeyError: env untouched
         return;
     }
     if (lane == 0) o.err[e] = 0;
-    __syncthreads();           // staged grid visible
+    if (mv) dir = nd;
+    const int ncell = mv ? (hr + dir_dr(dir)) * W + hc + dir_dc(dir) : -1 - lane;
+    __syncthreads();                       // staged grid + origins visible
 
-    // _check_collision :521-544, groups in first-appearance order
-    int death[MS], eat[MS], kills[MS], win[MS];
-#pragma unroll
-    for (int k = 0; k < MS; k++) death[k] = eat[k] = kills[k] = win[k] = 0;
-    int fruit_taken = 0, ndead = 0, alive_snakes = alive0;
-#pragma unroll
-    for (int g = 0; g < MS; g++) {
-        if (!mv[g]) continue;
-        bool lead = true;
-#pragma unroll
-        for (int k = 0; k < g; k++) lead &= !(mv[k] && ncell[k] == ncell[g]);
-        if (!lead) continue;
-        int cnt = 0;
-#pragma unroll
-        for (int k = 0; k < MS; k++) cnt += (mv[k] && ncell[k] == ncell[g]);
-        const int v = work[ncell[g]], cv = v % 10;
-        if (cnt > 1 || cv == C_WALL || cv == C_BODY || cv == C_HEAD) {
-#pragma unroll
-            for (int k = 0; k < MS; k++)
-                if (mv[k] && ncell[k] == ncell[g]) { death[k] = 1; alive[k] = 0; ndead++; }
-            if (cv == C_FRUIT) fruit_taken++;   // head-on on a fruit: fruit stays, one more spawns
-            if (cv == C_BODY || cv == C_HEAD) {
-                const int own = v / 10;         // kill credit to the owner, self included
-#pragma unroll
-                for (int k = 0; k < MS; k++) kills[k] += (k == own);
-            }
-        } else if (cv == C_FRUIT) {
-            eat[g] = 1;
-            fruit_taken++;
-        }
+    // _check_collision :521-544 -- groups of snakes with the same target cell
+    int cnt = 0;
+    bool lower = false;
+    for (int j = 0; j < S; j++) {
+        const bool same = bcast(ncell, j) == ncell;
+        cnt += same;
+        lower |= same && j < lane;
     }
-    alive_snakes -= ndead;                                         // :334
+    const bool leader = mv && !lower;
+    const int v = mv ? work[ncell] : 0;
+    const int vid = div10(v), cv = v - 10 * vid;
+    const bool deadly = mv && (cnt > 1 || cv == C_WALL || cv == C_BODY || cv == C_HEAD);
+    const bool eat = mv && !deadly && cv == C_FRUIT;
+    // every target group on a fruit cell counts once: an eater, or a head-on there
+    // (the fruit stays and one more spawns)
+    const int fruit_taken = __popcll(__ballot(leader && cv == C_FRUIT));
+    // kill credit: one per deadly group on a BODY/HEAD cell, to its owner (self too)
+    const int owner = (leader && deadly && (cv == C_BODY || cv == C_HEAD)) ? vid : -1;
+    int kills = 0;
+    for (int j = 0; j < S; j++) kills += bcast(owner, j) == lane;
+    int alive_snakes = alive0 - __popcll(__ballot(deadly));                  // :334
+    bool death = deadly;
     // :338-346 a fruit eater's tail does not move: snakes entering it die (again)
-#pragma unroll
-    for (int g = 0; g < MS; g++) {
-        if (!eat[g]) continue;
-        const int tcell = tr[g] * W + tc[g];
-#pragma unroll
-        for (int k = 0; k < MS; k++) {
-            if (mv[k] && ncell[k] == tcell) {
-                death[k] = 1; alive[k] = 0; alive_snakes--; kills[g]++;
-            }
-        }
+    const int etail = eat ? tr * W + tc : -2;
+    bool hit = false;
+    for (int j = 0; j < S; j++) {
+        hit |= mv && bcast(etail, j) == ncell;
+        kills += (eat && bcast(ncell, j) == etail) ? 1 : 0;
     }
-    if (alive_snakes == 1 && S > 1) {                              // :347-352
-        bool found = false;
-#pragma unroll
-        for (int k = 0; k < MS; k++)
-            if (!found && k < S && alive[k]) { win[k] = 1; found = true; }
+    alive_snakes -= __popcll(__ballot(hit));
+    death |= hit;
+    alive = mv && !death;
+    const unsigned long long am = __ballot(isn && alive);
+    const bool win = alive_snakes == 1 && S > 1 && am && lane == __ffsll((long long)am) - 1;
+
+    // rewards, fp64 in the reference order (:354-370)
+    const bool counted = death || alive;   // not previously dead
+    double rew = 0.0;
+    if (counted) {
+        double r = c.rt * (double)alive;
+        r += c.rf * (double)eat;
+        r += c.rl * (double)death;
+        r += c.rk * (double)kills;
+        r += c.rw * (double)win;
+        rew = r;
     }
 
-    // rewards (fp64, reference order) + _update_grid in snake order (:354-374)
-    double rew[MS];
-    int dn[MS];
-    unsigned dying = 0;
-    uint8_t *ring = st.body + (int64_t)e * S * cap;
-#pragma unroll
-    for (int k = 0; k < MS; k++) {
-        rew[k] = 0.0; dn[k] = 1;
-        if (k >= S) continue;
-        if (death[k] || alive[k]) {
-            double r = c.rt * (double)alive[k];
-            r += c.rf * (double)eat[k];
-            r += c.rl * (double)death[k];
-            r += c.rk * (double)kills[k];
-            r += c.rw * (double)win[k];
-            rew[k] = r;
-            const int id = 10 * k;
-            if (alive[k]) {
-                work[hr[k] * W + hc[k]] = (uint8_t)(C_BODY + id);
-                hr[k] += dir_dr(dir[k]); hc[k] += dir_dc(dir[k]);
-                rh[k] = (rh[k] - 1) & (cap - 1);                   // directions.appendleft
-                if (lane == 0) ring[(int64_t)k * cap + rh[k]] = (uint8_t)dir[k];
-                rl[k]++;
-                if (!eat[k]) {                                     // directions.pop()
-                    const int pt = tr[k] * W + tc[k];
-                    tr[k] += dir_dr(tdir[k]); tc[k] += dir_dc(tdir[k]);
-                    rl[k]--;
-                    if (work[pt] == C_TAIL + id) work[pt] = C_EMPTY;
-                }
-                work[hr[k] * W + hc[k]] = (uint8_t)(C_HEAD + id);
-                work[tr[k] * W + tc[k]] = (uint8_t)(C_TAIL + id);
-            } else {
-                // dying: the tail is erased only while it is still this snake's
-                // (:561-563); the rest of the body is erased below (no other
-                // snake writes those cells this step).
-                const int tcell = tr[k] * W + tc[k];
-                if (work[tcell] / 10 == k) work[tcell] = C_EMPTY;
-                dying |= 1u << k;
-            }
-        }
-        dn[k] = !alive[k];
+    // _update_grid in two phases. Phase 1: every tail that leaves its cell is
+    // cleared if it still holds this snake's TAIL, and every dying snake's tail
+    // if it is still this snake's; phase 2: BODY at the old head, HEAD at the
+    // new head, TAIL at the new tail. Phase-2 cells are pairwise distinct and a
+    // phase-1 cell is rewritten in phase 2 only by a snake entering that tail,
+    // which is what the reference's index-ordered updates produce.
+    const int pt = tr * W + tc;
+    if (alive && !eat) {
+        if (work[pt] == C_TAIL + 10 * lane) work[pt] = C_EMPTY;
     }
-    __syncthreads();
-    // draw(grid, coords, EMPTY) for the dying snakes: coords = head - prefix sums
-    // of the direction deque (core/snake.py:86-94), one 64-cell chunk per pass.
-    while (dying) {
-        const int k = __ffs(dying) - 1;
-        dying &= dying - 1;
-        const int khr = pick<MS>(hr, k), khc = pick<MS>(hc, k);
-        const int krh = pick<MS>(rh, k), krl = pick<MS>(rl, k);
+    if (isn && death) {
+        if (div10(work[pt]) == lane) work[pt] = C_EMPTY;
+    }
+    wave_sync();
+    int nhr = hr, nhc = hc, ntr = tr, ntc = tc;
+    if (alive) {
+        work[hr * W + hc] = (uint8_t)(C_BODY + 10 * lane);
+        nhr = hr + dir_dr(dir);
+        nhc = hc + dir_dc(dir);
+        rh = (rh - 1) & (cap - 1);                                   // directions.appendleft
+        ring[rh] = (uint8_t)dir;
+        if (!eat) { ntr = tr + dir_dr(tdir); ntc = tc + dir_dc(tdir); }   // directions.pop()
+        else rl++;
+        work[nhr * W + nhc] = (uint8_t)(C_HEAD + 10 * lane);
+        work[ntr * W + ntc] = (uint8_t)(C_TAIL + 10 * lane);
+    }
+    wave_sync();
+    // draw(grid, coords, EMPTY) of each dying snake's head and body (the tail was
+    // handled above): coords = head - prefix sums of the direction deque
+    // (core/snake.py:86-94), 64 cells per pass.
+    unsigned long long dm = __ballot(isn && death);
+    while (dm) {
+        const int k = __ffsll((long long)dm) - 1;
+        dm &= dm - 1;
+        const int khr = bcast(hr, k), khc = bcast(hc, k), krh = bcast(rh, k), krl = bcast(rl, k);
+        const uint8_t *kring = st.body + ((int64_t)e * S + k) * cap;
         int br = khr, bc = khc;
         if (lane == 0) work[khr * W + khc] = C_EMPTY;
         for (int m0 = 0; m0 < krl - 1; m0 += kWave) {
             const int m = m0 + lane;
             const bool ok = m < krl - 1;
-            const int d = ok ? ring[(int64_t)k * cap + ((krh + m) & (cap - 1))] : 0;
+            const int d = ok ? kring[(krh + m) & (cap - 1)] : 0;
             const int sr = wave_scan(ok ? dir_dr(d) : 0, lane);
             const int sc = wave_scan(ok ? dir_dc(d) : 0, lane);
             if (ok) work[(br - sr) * W + (bc - sc)] = C_EMPTY;
-            br -= __shfl(sr, 63);
-            bc -= __shfl(sc, 63);
+            br -= bcast(sr, 63);
+            bc -= bcast(sc, 63);
         }
     }
-    __syncthreads();
+    wave_sync();
 
     WaveMT mt;
     bool mt_loaded = false;
@@ -655,80 +607,74 @@ __global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
         place_fruits(c, work, mt, fruit_taken, fbuf, lane);
     }
 
-    // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412);
-    // lane k owns snake k.
-    const bool me = lane < S;
-    const int ks = me ? lane : 0;
-    const double myrew = pick<MS>(rew, ks);
-    const int myd = pick<MS>(dn, ks);
-    const int myfr = pick<MS>(eat, ks);
-    const int mykl = pick<MS>(kills, ks);
-    const int mydeath = pick<MS>(death, ks);
-    const int myalive = pick<MS>(alive, ks);
-    const bool counted = mydeath || myalive;                       // not previously dead
+    // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
+    const int dn = !alive;
     double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     double *sp = st.stats + (int64_t)e * 4 * S;
-    if (me) {
+    if (isn) {
         s0 = sp[lane]; s1 = sp[S + lane]; s2 = sp[2 * S + lane]; s3 = sp[3 * S + lane];
-        const double msk = 1.0 - (double)myd;
-        s0 = s0 + msk * myrew;
+        const double msk = 1.0 - (double)dn;
+        s0 = s0 + msk * rew;
         s1 = s1 + msk * 1.0;
-        s2 = s2 + msk * (counted ? (double)myfr : 0.0);
-        s3 = s3 + msk * (counted ? (double)mykl : 0.0);
+        s2 = s2 + msk * (counted ? (double)eat : 0.0);
+        s3 = s3 + msk * (counted ? (double)kills : 0.0);
     }
     const int eplen1 = eplen + 1;
-    int fd = ((double)eplen1 >= c.max_steps) ? 1 : myd;
-    const unsigned long long done_m = __ballot(me && fd);
+    int fd = ((double)eplen1 >= c.max_steps) ? 1 : dn;
+    const unsigned long long done_m = __ballot(isn && fd);
     const unsigned long long all_m = (S >= 64) ? ~0ull : ((1ull << S) - 1ull);
     const bool ep_end = c.coop ? (done_m != 0ull) : (done_m == all_m);
     if (c.coop && ep_end) fd = 1;
-    if (me) {
-        o.rew[(int64_t)e * S + lane] = myrew;
+    if (isn) {
+        o.rew[(int64_t)e * S + lane] = rew;
         o.done[(int64_t)e * S + lane] = (uint8_t)fd;
     }
     if (lane == 0) o.ep_done[e] = ep_end ? 1 : 0;
     if (ep_end) {
         int rank = 1;
         for (int j = 0; j < S; j++) rank += (__shfl(s0, j) > s0);
-        if (me) {
+        if (isn) {
             o.rank[(int64_t)e * S + lane] = rank;
             double *es = o.ep_stats + (int64_t)e * 4 * S;
             es[lane] = s0; es[S + lane] = s1; es[2 * S + lane] = s2; es[3 * S + lane] = s3;
         }
         s0 = s1 = s2 = s3 = 0.0;                                   // _reset_epi_stats
     }
-    if (me) { sp[lane] = s0; sp[S + lane] = s1; sp[2 * S + lane] = s2; sp[3 * S + lane] = s3; }
+    if (isn) { sp[lane] = s0; sp[S + lane] = s1; sp[2 * S + lane] = s2; sp[3 * S + lane] = s3; }
 
     if (ep_end && c.autoreset) {   // vector-env auto-reset (wrappers.py:139-145)
         if (!mt_loaded) mt_load(mt, st.mt + (int64_t)e * kMtN, mtpos, lane);
-        __syncthreads();
+        __builtin_amdgcn_s_setprio(3);      // a reset is ~100x a step: let it run ahead
         do_reset<MS>(c, st, o, e, mt, lds, lane);
+        __builtin_amdgcn_s_setprio(0);
         return;
     }
 
-    // commit the new grid into the ring slot of the dropped frame
-    const int ncur = (c.fs == 1) ? 0 : (cur + 1) % c.fs;
-    copy_lds_to_global(st.grid + ((int64_t)e * c.fs + ncur) * c.grid_stride, work, c.grid_stride, lane);
-    if (me) {
-        int4 rec;
-        rec.x = pick<MS>(hr, lane) | (pick<MS>(hc, lane) << 8) |
-                (pick<MS>(tr, lane) << 16) | (pick<MS>(tc, lane) << 24);
-        rec.y = pick<MS>(dir, lane) | (myalive << 8);
-        rec.z = pick<MS>(rh, lane) | (pick<MS>(rl, lane) << 16);
-        rec.w = 0;
-        reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + lane] = rec;
+    // commit: new grid into the ring slot of the dropped frame, records, centres
+    const int ncur = (fs == 1) ? 0 : (cur + 1) % fs;
+    uint8_t *gdst = st.grid + ((int64_t)e * fs + ncur) * c.grid_stride;
+    for (int q = lane; q < n16; q += kWave)
+        reinterpret_cast<uint4 *>(gdst)[q] = reinterpret_cast<const uint4 *>(work)[q];
+    // crop centre = the own HEAD cell: the new head while alive, (0,0) when dead
+    const int chr = alive ? nhr : 0, chc = alive ? nhc : 0;
+    if (isn) {
+        int4 nrec;
+        nrec.x = nhr | (nhc << 8) | (ntr << 16) | (ntc << 24);
+        nrec.y = dir | (alive << 8);
+        nrec.z = rh | (rl << 16);
+        nrec.w = 0;
+        reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + lane] = nrec;
+        org[(fs - 1) * kMaxSnakes + lane] = pack_origin(c, chr, chc);
+        if (fs > 1) st.ctr[((int64_t)e * fs + ncur) * S + lane] = (uint16_t)((chr << 8) | chc);
     }
     if (lane == 0) {
-        er[ENV_ALIVE] = alive_snakes;
-        er[ENV_EPLEN] = eplen1;
-        er[ENV_CUR] = ncur;
-        er[ENV_MTPOS] = mt_loaded ? mt.pos : mtpos;
+        int4 ner;
+        ner.x = alive_snakes; ner.y = eplen1; ner.z = ncur; ner.w = mt_loaded ? mt.pos : mtpos;
+        *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = ner;
     }
     if (mt_loaded) mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
-    if (c.vr) {
-        for (int x = 0; x < c.fs; x++) find_centers(c, frames + x * c.grid_stride, ctr + x * kMaxSnakes, lane);
-    }
-    encode(c, frames, ctr, o.obs + (int64_t)e * c.units * 8, lane);
+    wave_sync();
+    encode(c, frames, org, o.obs + (int64_t)e * c.units * 8, lane);
 }
 
 template <int MS>

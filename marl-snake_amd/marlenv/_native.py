@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 1
+SNAKE_ABI_VERSION = 2
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
@@ -30,7 +30,7 @@ class SnakeCfg(ctypes.Structure):
 
 class SnakeLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
-        'grid', 'snake', 'body', 'env', 'stats', 'mt', 'cand', 'jscratch', 'obs', 'rew', 'done',
+        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'obs', 'rew', 'done',
         'ep_done', 'rank', 'ep_stats', 'err', 'n_cand')] + [
         ('obs_h', ctypes.c_int32), ('obs_w', ctypes.c_int32), ('obs_c', ctypes.c_int32),
         ('grid_stride', ctypes.c_int32), ('ring_cap', ctypes.c_int32)]
@@ -38,7 +38,7 @@ class SnakeLayout(ctypes.Structure):
 
 class SnakeState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
-        'grid', 'snake', 'body', 'env', 'stats', 'mt', 'cand', 'jscratch')]
+        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch')]
 
 
 class SnakeOut(ctypes.Structure):
@@ -58,6 +58,11 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # PyTorch owns device memory and streams: its HIP runtime must be the one in
+    # the process before libsnake_amd.so resolves libamdhip64.so.7 (loading ours
+    # first brings in /opt/rocm's copy beside torch's, and launches then fail
+    # with "no ROCm-capable device").
+    import torch  # noqa: F401
     if not os.path.exists(LIB_PATH):
         raise NativeError(f'{LIB_PATH} not built: run `python __graft_entry__.py` '
                           '(hipcc --offload-arch=gfx950); there is no CPU fallback')

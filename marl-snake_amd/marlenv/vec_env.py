@@ -61,6 +61,7 @@ class SnakeVecEnv:
         self.snake = buf(lay.snake, torch.int32)
         self.body = buf(lay.body)
         self.env_rec = buf(lay.env, torch.int32)
+        self.ctr = buf(lay.ctr, torch.int16)
         self.stats = buf(lay.stats, torch.float64)
         self.mt = buf(lay.mt, torch.int32)
         self.jscratch = buf(lay.jscratch, torch.int16) if lay.jscratch else None
@@ -71,7 +72,7 @@ class SnakeVecEnv:
         self.cand = torch.from_numpy(host).to(dev)
         self._state = SnakeState(
             self.grid.data_ptr(), self.snake.data_ptr(), self.body.data_ptr(), self.env_rec.data_ptr(),
-            self.stats.data_ptr(), self.mt.data_ptr(), self.cand.data_ptr(),
+            self.ctr.data_ptr(), self.stats.data_ptr(), self.mt.data_ptr(), self.cand.data_ptr(),
             self.jscratch.data_ptr() if self.jscratch is not None else None)
         check(L.snake_seed(ctypes.byref(self.cfg), ctypes.byref(self._state), N, self.seed_base,
                            self.env_offset, self._stream()))
@@ -210,6 +211,15 @@ class SnakeVecEnv:
             x = hr | (hc << 8) | (tr << 16) | (tc << 24)
             rec[k] = [x - (1 << 32) if x >= (1 << 31) else x, dirs[0] | (int(bool(alive)) << 8),
                       (len(co) - 1) << 16, 0]
+        # crop centres of the refilled frames: the own HEAD cell (argmax of the own
+        # head plane, snake_env.py:500-501), (0, 0) when there is none
+        g2 = np.asarray(grid, np.int64).reshape(H, W)
+        ctr = np.zeros(S, np.int16)
+        for k in range(S):
+            hits = np.argwhere(g2 == 3 + 10 * k)
+            if len(hits):
+                ctr[k] = (int(hits[0][0]) << 8) | int(hits[0][1])
+        self.ctr.view(self.num_envs, fs * S)[i].copy_(torch.from_numpy(np.tile(ctr, fs)).to(self.device))
         self.snake.view(self.num_envs, S * 4)[i].copy_(torch.from_numpy(rec.reshape(-1)).to(self.device))
         self.body.view(self.num_envs, S * lay.ring_cap)[i].copy_(torch.from_numpy(body.reshape(-1)).to(self.device))
         er = self.env_rec.view(self.num_envs, 8)

@@ -24,6 +24,11 @@ for s in "$@"; do
         bench) step bench 600 python bench.py ;;
         benchq) step bench 300 python bench.py --steps 200 --warmup 50 --cpu-seconds 5 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 50 --no-cpu-baseline ;;
+        probe) step probe 600 python scripts/perf_probe.py ;;
+        pmc) step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc1 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
+             step pmc2 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc2 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
+             step pmc3 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc3 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
+             step pmc4 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc4 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
