@@ -196,7 +196,10 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->stats = N * 4 * S * 8;
     o->mt = N * kMtN * 4;
     o->cand = o->n_cand * c->snake_length * 2;
-    o->jscratch = (o->n_cand * 2 <= kJarrLdsMax) ? 0 : N * o->n_cand * 2;
+    // Fisher-Yates draw record of a reset: global scratch, L2-resident while used.
+    // (Kept out of LDS so the step kernel's LDS, and with it its occupancy, stays
+    // at the grid ring + a few hundred bytes.)
+    o->jscratch = N * o->n_cand * 2;
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
     o->done = N * S;
@@ -236,6 +239,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->units = k->S * k->oh * k->ow * k->fs;
     k->grid_stride = lay.grid_stride; k->ring_cap = lay.ring_cap; k->n_cand = (int)lay.n_cand;
     k->cs = (k->HW + kWave - 1) / kWave;
+    k->ring_bytes = k->fs * k->grid_stride;
     // 128 units in mixed radix (f: fs, j: ow, i: oh, k: S)
     int64_t a = 128;
     k->adv_f = (int)(a % k->fs); a /= k->fs;
@@ -246,10 +250,14 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->lds_frames = off; off += (int)round_up((int64_t)k->fs * k->grid_stride, 16);
     k->lds_centers = off; off += (int)round_up(4 * k->fs * kMaxSnakes, 16);
     k->lds_fruit = off; off += (int)round_up(2 * kMaxFruits, 16);
-    k->jarr_in_lds = lay.jscratch == 0;
+    k->jarr_in_lds = 0;
     k->lds_jarr = off;
     if (k->jarr_in_lds) off += (int)round_up(2 * (int64_t)k->n_cand, 16);
     k->lds_bytes = off;
+    if (k->lds_bytes > 64 * 1024) {
+        set_error("grid ring of %d bytes per env does not fit the LDS budget", k->ring_bytes);
+        return SNAKE_E_CONFIG;
+    }
     k->rf = c->rew_fruit; k->rk = c->rew_kill; k->rl = c->rew_lose; k->rw = c->rew_win;
     k->rt = c->rew_time; k->max_steps = c->max_episode_steps;
     return SNAKE_OK;

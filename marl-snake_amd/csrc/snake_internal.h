@@ -12,7 +12,6 @@ constexpr int kMtN = 624;
 constexpr int kMaxSnakes = 16;
 constexpr int kMaxFruits = 64;
 constexpr int kEnvRec = 8;          // int32 words per env record
-constexpr int kJarrLdsMax = 16384;  // bytes of reset scratch kept in LDS
 
 // env record words
 enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3 };
@@ -24,6 +23,7 @@ struct KCfg {
     int oh, ow, units;          // units = S*oh*ow*fs (one unit = 8 obs bytes)
     int grid_stride, ring_cap, n_cand;
     int cs;                     // cells per lane when a wave sweeps the grid
+    int ring_bytes;             // fs * grid_stride (the grid ring of one env)
     // step of 128 units expressed in the mixed radix (fs, ow, oh, S)
     int adv_f, adv_j, adv_i, adv_k;
     // dynamic LDS carve (bytes, 16-aligned)

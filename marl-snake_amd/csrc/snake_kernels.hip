@@ -104,39 +104,60 @@ __device__ __forceinline__ void mt_store(const WaveMT &m, uint32_t *g, int lane)
 // mt19937_gen, wave-parallel. new[i] = X ^ (y >> 1) ^ mag(y), y = old[i]|old[i+1]
 // (upper/lower bits), X = old[i+397] for i < 227 and new[i-227] after; the last
 // word mixes new[0]. Every element's inputs sit at a fixed lane offset (13 for
-// i+397, 29 for i-227) of an earlier register, so the twist is 10 register steps.
+// i+397, 29 for i-227) of an earlier register, so the twist is 10 register
+// steps in four dependency levels (registers {0-2}, {3-5}, {6-8}, {9}); the
+// cross-lane reads of a level are issued together.
+__device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t x)
+{
+    const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+    return x ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
 __device__ void mt_twist(WaveMT &m, int lane)
 {
-    constexpr uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, MATA = 0x9908b0dfu;
-    uint32_t nw[10];
     const int l1 = (lane + 1) & 63, l13 = (lane + 13) & 63, l29 = (lane + 29) & 63;
+    const bool wrap13 = lane + 13 >= 64, wrap29 = lane + 29 >= 64;
+    uint32_t o1[10], xo[4], nw[10];
+    // level 0: everything that reads old words only
 #pragma unroll
     for (int t = 0; t < 10; t++) {
-        const int e = 64 * t + lane;
-        const uint32_t cur = m.w[t];
-        const uint32_t same = __shfl(cur, l1);
+        const uint32_t same = __shfl(m.w[t], l1);
         const uint32_t nxt = __builtin_amdgcn_readlane(m.w[t < 9 ? t + 1 : 9], 0);
-        uint32_t o1 = (lane == 63) ? nxt : same;
-        uint32_t xold = 0, xnew = 0;
-        if (t <= 3) {
-            const uint32_t a = __shfl(m.w[t + 6 <= 9 ? t + 6 : 9], l13);
-            const uint32_t b = __shfl(m.w[t + 7 <= 9 ? t + 7 : 9], l13);
-            xold = (lane + 13 < 64) ? a : b;
-        }
-        if (t >= 3) {
+        o1[t] = (lane == 63) ? nxt : same;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const uint32_t a = __shfl(m.w[t + 6], l13);
+        const uint32_t b = __shfl(m.w[t + 7 <= 9 ? t + 7 : 9], l13);
+        xo[t] = wrap13 ? b : a;
+    }
+#pragma unroll
+    for (int t = 0; t < 3; t++) nw[t] = mt_mix(m.w[t], o1[t], xo[t]);
+    // levels 1..3: X = new[i-227] = register t-4 (or t-3 past the lane wrap)
+#pragma unroll
+    for (int lv = 1; lv <= 3; lv++) {
+        const int t0 = 3 * lv, t1 = (lv == 3) ? 10 : 3 * lv + 3;
+        uint32_t xn[3];
+#pragma unroll
+        for (int t = t0; t < t1; t++) {
             const uint32_t a = __shfl(nw[t >= 4 ? t - 4 : 0], l29);
-            const uint32_t b = __shfl(nw[t - 3 >= 0 ? t - 3 : 0], l29);
-            xnew = (lane + 29 < 64) ? a : b;
+            const uint32_t b = __shfl(nw[t - 3], l29);
+            xn[t - t0] = wrap29 ? b : a;
         }
-        uint32_t x = (e < 227) ? xold : xnew;
-        if (t == 9) {
-            const uint32_t n0 = __builtin_amdgcn_readlane(nw[0], 0);
-            const uint32_t n396 = __builtin_amdgcn_readlane(nw[6], 12);
-            if (e == kMtN - 1) { o1 = n0; x = n396; }
+        uint32_t n0 = 0, n396 = 0;
+        if (lv == 3) {
+            n0 = __builtin_amdgcn_readlane(nw[0], 0);
+            n396 = __builtin_amdgcn_readlane(nw[6], 12);
         }
-        const uint32_t y = (cur & UPPER) | (o1 & LOWER);
-        const uint32_t v = x ^ (y >> 1) ^ ((y & 1u) ? MATA : 0u);
-        nw[t] = (e < kMtN) ? v : 0u;
+#pragma unroll
+        for (int t = t0; t < t1; t++) {
+            const int e = 64 * t + lane;
+            uint32_t x = xn[t - t0], nx = o1[t];
+            if (t == 3) x = (e < 227) ? xo[3] : x;
+            if (t == 9 && e == kMtN - 1) { nx = n0; x = n396; }
+            const uint32_t v = mt_mix(m.w[t], nx, x);
+            nw[t] = (e < kMtN) ? v : 0u;
+        }
     }
 #pragma unroll
     for (int t = 0; t < 10; t++) m.w[t] = nw[t];
@@ -214,35 +235,44 @@ __device__ void mt_perm_draws(WaveMT &m, int n, uint16_t *jarr, int lane)
 }
 
 // Final arr[k] of the Fisher-Yates pass for k < S: walk each position
-// backwards through the swaps (i ascending = reverse of the draw order). A
-// chunk of 64 swaps that touches none of the S tracked positions costs one
-// ballot.
+// backwards through the swaps (i ascending = reverse of the draw order). Two
+// chunks of 64 swaps are read together; a pair that touches none of the S
+// tracked positions costs one ballot.
+template <int MS>
+__device__ __forceinline__ void trace_chunk(int b, int n, int jv, int S, int (&q)[MS], int lane)
+{
+    const int i = b + lane;
+#pragma unroll
+    for (int k = 0; k < MS; k++) {
+        if (k >= S) continue;
+        int from = -1;
+        for (;;) {
+            const unsigned long long mk = __ballot(i < n && lane > from && (i == q[k] || jv == q[k]));
+            if (!mk) break;
+            const int f = __ffsll((long long)mk) - 1;
+            const int jf = bcast(jv, f);
+            q[k] = (b + f == q[k]) ? jf : b + f;
+            from = f;
+        }
+    }
+}
+
 template <int MS>
 __device__ void perm_trace(int n, const uint16_t *jarr, int S, int (&q)[MS], int lane)
 {
 #pragma unroll
     for (int k = 0; k < MS; k++) q[k] = k;
-    for (int b = 1; b < n; b += kWave) {
-        const int i = b + lane;
-        const int jv = (i < n) ? (int)jarr[i] : -1;
+    for (int b0 = 1; b0 < n; b0 += 2 * kWave) {
+        const int i0 = b0 + lane, i1 = i0 + kWave;
+        const int j0 = (i0 < n) ? (int)jarr[i0] : -1;
+        const int j1 = (i1 < n) ? (int)jarr[i1] : -1;
         bool hit = false;
 #pragma unroll
-        for (int k = 0; k < MS; k++) hit |= (k < S) && (i == q[k] || jv == q[k]);
-        if (__ballot(hit && i < n) == 0ull) continue;
-#pragma unroll
-        for (int k = 0; k < MS; k++) {
-            if (k >= S) continue;
-            int from = -1;
-            for (;;) {
-                const unsigned long long mk =
-                    __ballot(i < n && lane > from && (i == q[k] || jv == q[k]));
-                if (!mk) break;
-                const int f = __ffsll((long long)mk) - 1;
-                const int jf = bcast(jv, f);
-                q[k] = (b + f == q[k]) ? jf : b + f;
-                from = f;
-            }
-        }
+        for (int k = 0; k < MS; k++)
+            hit |= (k < S) && ((i0 < n && (i0 == q[k] || j0 == q[k])) || (i1 < n && (i1 == q[k] || j1 == q[k])));
+        if (__ballot(hit) == 0ull) continue;
+        trace_chunk<MS>(b0, n, j0, S, q, lane);
+        trace_chunk<MS>(b0 + kWave, n, j1, S, q, lane);
     }
 }
 
@@ -292,36 +322,42 @@ __device__ __forceinline__ unsigned long long onehot(int v, int k)
 }
 
 __device__ __forceinline__ unsigned long long unit_bits(const KCfg &c, const uint8_t *frames,
-                                                       const int *org, int k, int i, int j, int f)
+                                                       const int *org, int k, int i, int j, int s)
 {
-    const int p = org[f * kMaxSnakes + k];
+    const int p = org[s * kMaxSnakes + k];
     const int r = (p >> 16) - 256 + i, cc = (p & 0xffff) - 256 + j;
     if ((unsigned)r >= (unsigned)c.H || (unsigned)cc >= (unsigned)c.W) return 0ull;
-    return onehot(frames[f * c.grid_stride + r * c.W + cc], k);
+    return onehot(frames[s * c.grid_stride + r * c.W + cc], k);
 }
 
-// obs layout (S, oh, ow, 8*fs): unit u = ((k*oh + i)*ow + j)*fs + f is 8 bytes.
+// obs layout (S, oh, ow, 8*fs): unit u = ((k*oh + i)*ow + j)*fs + f is 8 bytes;
+// frame f (oldest first) is ring slot (slot0 + f) % fs of the LDS ring.
 // Lane l writes units 2l, 2l+1 (16 bytes) then strides by 128 units; the
 // (k,i,j,f) digits advance by carries, no division in the loop.
-__device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, uint8_t *obs_env, int lane)
+__device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int slot0,
+                       uint8_t *obs_env, int lane)
 {
-    const int U = c.units, pairs = (U + 1) >> 1;
+    const int U = c.units, pairs = (U + 1) >> 1, fs = c.fs;
     int u = 2 * lane;
-    int f = u % c.fs, rest = u / c.fs;
+    int f = u % fs, rest = u / fs;
     int j = rest % c.ow;
     rest /= c.ow;
     int i = rest % c.oh;
     int k = rest / c.oh;
     const bool wide = (U & 1) == 0;
     for (int p = lane; p < pairs; p += kWave) {
-        const unsigned long long a = unit_bits(c, frames, org, k, i, j, f);
+        int s = slot0 + f;
+        s -= (s >= fs) ? fs : 0;
+        const unsigned long long a = unit_bits(c, frames, org, k, i, j, s);
         int f2 = f + 1, j2 = j, i2 = i, k2 = k;
-        if (f2 == c.fs) {
+        if (f2 == fs) {
             f2 = 0;
             if (++j2 == c.ow) { j2 = 0; if (++i2 == c.oh) { i2 = 0; k2++; } }
         }
+        int s2 = slot0 + f2;
+        s2 -= (s2 >= fs) ? fs : 0;
         const bool has_b = 2 * p + 1 < U;
-        const unsigned long long b = has_b ? unit_bits(c, frames, org, k2, i2, j2, f2) : 0ull;
+        const unsigned long long b = has_b ? unit_bits(c, frames, org, k2, i2, j2, s2) : 0ull;
         if (wide) {
             uint4 v;
             v.x = (uint32_t)a; v.y = (uint32_t)(a >> 32);
@@ -332,7 +368,7 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, uin
             if (has_b) *reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p + 8) = b;
         }
         f += c.adv_f;
-        if (f >= c.fs) { f -= c.fs; j++; }
+        if (f >= fs) { f -= fs; j++; }
         j += c.adv_j;
         if (j >= c.ow) { j -= c.ow; i++; }
         i += c.adv_i;
@@ -396,6 +432,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     wave_sync();
     const int nxt = __shfl(cell, (lane + 1) & 63);
     const int tailcell = __shfl(cell, min(lane + L - 1, 63));
+    const int pretail = __shfl(cell, min(lane + L - 2, 63));
     if (lane < SL) {
         const int v = (si == 0 ? C_HEAD : (si == L - 1 ? C_TAIL : C_BODY)) + 10 * sk;
         work[cell] = (uint8_t)v;
@@ -407,7 +444,8 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
             rec.x = hr | (hc << 8) | (tr << 16) | (tc << 24);
             rec.y = dir_of_diff(cell - nxt, W) | (1 << 8);
             rec.z = 0 | ((L - 1) << 16);
-            rec.w = 0;
+            // cached directions[-1] (the direction move() pops next)
+            rec.w = dir_of_diff(pretail - tailcell, W);
             reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + sk] = rec;
             const int og = pack_origin(c, hr, hc);
             for (int f = 0; f < c.fs; f++) {
@@ -433,54 +471,67 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     if (lane < 4 * S) st.stats[(int64_t)e * 4 * S + lane] = 0.0;   // _reset_epi_stats
     mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
     wave_sync();
-    encode(c, frames, org, o.obs + (int64_t)e * c.units * 8, lane);
+    encode(c, frames, org, 0, o.obs + (int64_t)e * c.units * 8, lane);
 }
 
 // -------------------------------------------------------------------- step
+// Copy bytes [0, n) (n % 16 == 0) global -> LDS, 16 B per lane, up to four
+// loads in flight per lane before the LDS writes.
+__device__ __forceinline__ void stage_to_lds(uint8_t *dst, const uint8_t *src, int n, int lane)
+{
+    const int n16 = n >> 4;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    for (int q = lane; q < n16; q += 4 * kWave) {
+        const int q1 = q + kWave, q2 = q + 2 * kWave, q3 = q + 3 * kWave;
+        const uint4 a = s4[q];
+        const uint4 b = q1 < n16 ? s4[q1] : a;
+        const uint4 c = q2 < n16 ? s4[q2] : a;
+        const uint4 d = q3 < n16 ? s4[q3] : a;
+        d4[q] = a;
+        if (q1 < n16) d4[q1] = b;
+        if (q2 < n16) d4[q2] = c;
+        if (q3 < n16) d4[q3] = d;
+    }
+}
+
 template <int MS>
-__global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
+__global__ void __launch_bounds__(64, 8) k_step(const KCfg c, const snake_state st,
                                              const int8_t *__restrict__ actions, const snake_out o)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int e = blockIdx.x, lane = threadIdx.x;
-    const int S = c.S, W = c.W, cap = c.ring_cap, fs = c.fs;
-    uint8_t *frames = lds + c.lds_frames;
+    const int S = c.S, W = c.W, cap = c.ring_cap, fs = c.fs, stride = c.grid_stride;
+    uint8_t *frames = lds + c.lds_frames;                  // ring slots, slot order
     int *org = reinterpret_cast<int *>(lds + c.lds_centers);
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
-    uint8_t *work = frames + (fs - 1) * c.grid_stride;
-    const int4 er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
-    const int alive0 = er.x, eplen = er.y, cur = er.z, mtpos = er.w;
     const bool isn = lane < S;
 
-    // snake k's record in lane k: head/tail coords, heading, alive, deque ring
+    // ---- every load this step needs, issued up front (one memory round trip)
+    const int4 er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
     int4 rec = make_int4(0, 0, 0, 0);
     int act = 0;
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    double *sp = st.stats + (int64_t)e * 4 * S;
     if (isn) {
         rec = reinterpret_cast<const int4 *>(st.snake)[(int64_t)e * S + lane];
         act = actions[(int64_t)e * S + lane];
+        s0 = sp[lane]; s1 = sp[S + lane]; s2 = sp[2 * S + lane]; s3 = sp[3 * S + lane];
     }
-    // Stage the grid ring: LDS frame x < fs-1 <- slot (cur+2+x) % fs (the fs-1
-    // most recent frames, oldest first); LDS frame fs-1 (work) <- slot cur.
-    const uint8_t *gbase = st.grid + (int64_t)e * fs * c.grid_stride;
-    const int n16 = c.grid_stride >> 4;
-    for (int x = 0; x < fs; x++) {
-        const int slot = (x == fs - 1) ? cur : (cur + 2 + x) % fs;
-        for (int q = lane; q < n16; q += kWave)
-            reinterpret_cast<uint4 *>(frames + x * c.grid_stride)[q] =
-                reinterpret_cast<const uint4 *>(gbase + slot * c.grid_stride)[q];
+    stage_to_lds(frames, st.grid + (int64_t)e * c.ring_bytes, c.ring_bytes, lane);
+    if (fs > 1) {                             // crop centres of every ring slot
+        for (int q = lane; q < fs * S; q += kWave) {
+            const int x = q / S, k = q - x * S;
+            const int p = st.ctr[(int64_t)e * fs * S + q];
+            org[x * kMaxSnakes + k] = pack_origin(c, p >> 8, p & 255);
+        }
     }
-    if (fs > 1 && lane < (fs - 1) * S) {      // crop origins of the kept older frames
-        const int x = lane / S, k = lane - x * S;
-        const int slot = (cur + 2 + x) % fs;
-        const int p = st.ctr[((int64_t)e * fs + slot) * S + k];
-        org[x * kMaxSnakes + k] = pack_origin(c, p >> 8, p & 255);
-    }
+    const int alive0 = er.x, eplen = er.y, cur = er.z, mtpos = er.w;
+    const int ncur = (fs == 1) ? 0 : (cur + 1 == fs ? 0 : cur + 1);
     int hr = rec.x & 255, hc = (rec.x >> 8) & 255, tr = (rec.x >> 16) & 255, tc = (rec.x >> 24) & 255;
     int dir = rec.y & 3, alive = (rec.y >> 8) & 1;
     int rh = rec.z & 0xffff, rl = (rec.z >> 16) & 0xffff;
-    uint8_t *ring = st.body + ((int64_t)e * S + lane) * cap;
-    // the tail direction move() pops (core/snake.py:103), prefetched
-    const int tdir = (isn && alive) ? ring[(rh + rl - 1) & (cap - 1)] : 0;
+    const int tdir = rec.w;                   // cached directions[-1] (core/snake.py:103)
 
     // snake_env.py:318-330 heading + target cell per alive snake
     const bool mv = isn && alive;
@@ -496,10 +547,16 @@ __global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
         if (lane == 0) o.err[e] = 1;       // action_angle_dict[action] KeyError: env untouched
         return;
     }
-    if (lane == 0) o.err[e] = 0;
     if (mv) dir = nd;
     const int ncell = mv ? (hr + dir_dr(dir)) * W + hc + dir_dc(dir) : -1 - lane;
-    __syncthreads();                       // staged grid + origins visible
+    // the new frame is built in the slot of the frame that leaves the stack
+    uint8_t *work = frames + ncur * stride;
+    if (fs > 1) {
+        wave_sync();
+        for (int q = lane; q < (stride >> 4); q += kWave)
+            reinterpret_cast<uint4 *>(work)[q] = reinterpret_cast<const uint4 *>(frames + cur * stride)[q];
+    }
+    wave_sync();
 
     // _check_collision :521-544 -- groups of snakes with the same target cell
     int cnt = 0;
@@ -562,15 +619,22 @@ __global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
         if (div10(work[pt]) == lane) work[pt] = C_EMPTY;
     }
     wave_sync();
-    int nhr = hr, nhc = hc, ntr = tr, ntc = tc;
+    uint8_t *ring = st.body + ((int64_t)e * S + lane) * cap;
+    int nhr = hr, nhc = hc, ntr = tr, ntc = tc, ntdir = tdir;
     if (alive) {
         work[hr * W + hc] = (uint8_t)(C_BODY + 10 * lane);
         nhr = hr + dir_dr(dir);
         nhc = hc + dir_dc(dir);
         rh = (rh - 1) & (cap - 1);                                   // directions.appendleft
         ring[rh] = (uint8_t)dir;
-        if (!eat) { ntr = tr + dir_dr(tdir); ntc = tc + dir_dc(tdir); }   // directions.pop()
-        else rl++;
+        if (!eat) {                                                  // directions.pop()
+            ntr = tr + dir_dr(tdir);
+            ntc = tc + dir_dc(tdir);
+            // next directions[-1]; with one direction left it is the one just pushed
+            ntdir = (rl == 1) ? dir : ring[(rh + rl - 1) & (cap - 1)];
+        } else {
+            rl++;
+        }
         work[nhr * W + nhc] = (uint8_t)(C_HEAD + 10 * lane);
         work[ntr * W + ntc] = (uint8_t)(C_TAIL + 10 * lane);
     }
@@ -609,10 +673,7 @@ __global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
 
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
     const int dn = !alive;
-    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    double *sp = st.stats + (int64_t)e * 4 * S;
     if (isn) {
-        s0 = sp[lane]; s1 = sp[S + lane]; s2 = sp[2 * S + lane]; s3 = sp[3 * S + lane];
         const double msk = 1.0 - (double)dn;
         s0 = s0 + msk * rew;
         s1 = s1 + msk * 1.0;
@@ -629,7 +690,7 @@ __global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
         o.rew[(int64_t)e * S + lane] = rew;
         o.done[(int64_t)e * S + lane] = (uint8_t)fd;
     }
-    if (lane == 0) o.ep_done[e] = ep_end ? 1 : 0;
+    if (lane == 0) { o.ep_done[e] = ep_end ? 1 : 0; o.err[e] = 0; }
     if (ep_end) {
         int rank = 1;
         for (int j = 0; j < S; j++) rank += (__shfl(s0, j) > s0);
@@ -650,21 +711,14 @@ __global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
         return;
     }
 
-    // commit: new grid into the ring slot of the dropped frame, records, centres
-    const int ncur = (fs == 1) ? 0 : (cur + 1) % fs;
-    uint8_t *gdst = st.grid + ((int64_t)e * fs + ncur) * c.grid_stride;
-    for (int q = lane; q < n16; q += kWave)
+    // commit the new frame into its ring slot; records; crop centres
+    uint8_t *gdst = st.grid + (int64_t)e * c.ring_bytes + ncur * stride;
+    for (int q = lane; q < (stride >> 4); q += kWave)
         reinterpret_cast<uint4 *>(gdst)[q] = reinterpret_cast<const uint4 *>(work)[q];
     // crop centre = the own HEAD cell: the new head while alive, (0,0) when dead
     const int chr = alive ? nhr : 0, chc = alive ? nhc : 0;
     if (isn) {
-        int4 nrec;
-        nrec.x = nhr | (nhc << 8) | (ntr << 16) | (ntc << 24);
-        nrec.y = dir | (alive << 8);
-        nrec.z = rh | (rl << 16);
-        nrec.w = 0;
-        reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + lane] = nrec;
-        org[(fs - 1) * kMaxSnakes + lane] = pack_origin(c, chr, chc);
+        org[ncur * kMaxSnakes + lane] = pack_origin(c, chr, chc);
         if (fs > 1) st.ctr[((int64_t)e * fs + ncur) * S + lane] = (uint16_t)((chr << 8) | chc);
     }
     if (lane == 0) {
@@ -674,7 +728,16 @@ __global__ void __launch_bounds__(64) k_step(const KCfg c, const snake_state st,
     }
     if (mt_loaded) mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
     wave_sync();
-    encode(c, frames, org, o.obs + (int64_t)e * c.units * 8, lane);
+    encode(c, frames, org, fs == 1 ? 0 : (ncur + 1 == fs ? 0 : ncur + 1),
+           o.obs + (int64_t)e * c.units * 8, lane);
+    if (isn) {      // last: the ring read for ntdir had the whole encode to land
+        int4 nrec;
+        nrec.x = nhr | (nhc << 8) | (ntr << 16) | (ntc << 24);
+        nrec.y = dir | (alive << 8);
+        nrec.z = rh | (rl << 16);
+        nrec.w = ntdir;
+        reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + lane] = nrec;
+    }
 }
 
 template <int MS>

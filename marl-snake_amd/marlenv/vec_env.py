@@ -54,7 +54,8 @@ class SnakeVecEnv:
         self.action_n = 5 if self.cfg.observer == 1 else 3
 
         def buf(nbytes, dtype=torch.uint8):
-            return torch.zeros(max(int(nbytes), 16), dtype=torch.uint8, device=dev).view(dtype)
+            n = int(nbytes)
+            return torch.zeros(max(n, 16), dtype=torch.uint8, device=dev)[:n].view(dtype)
 
         # state (layouts: include/snake_env.h snake_layout)
         self.grid = buf(lay.grid)
@@ -210,7 +211,7 @@ class SnakeVecEnv:
             (hr, hc), (tr, tc) = co[0], co[-1]
             x = hr | (hc << 8) | (tr << 16) | (tc << 24)
             rec[k] = [x - (1 << 32) if x >= (1 << 31) else x, dirs[0] | (int(bool(alive)) << 8),
-                      (len(co) - 1) << 16, 0]
+                      (len(co) - 1) << 16, dirs[-1]]
         # crop centres of the refilled frames: the own HEAD cell (argmax of the own
         # head plane, snake_env.py:500-501), (0, 0) when there is none
         g2 = np.asarray(grid, np.int64).reshape(H, W)

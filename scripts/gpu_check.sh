@@ -25,6 +25,7 @@ for s in "$@"; do
         benchq) step bench 300 python bench.py --steps 200 --warmup 50 --cpu-seconds 5 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 50 --no-cpu-baseline ;;
         probe) step probe 600 python scripts/perf_probe.py ;;
+        rlat) step rlat 300 python scripts/perf_probe.py --reset-latency ;;
         pmc) step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc1 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
              step pmc2 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc2 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
              step pmc3 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc3 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10

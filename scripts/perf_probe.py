@@ -53,11 +53,34 @@ def probe(N, S, kw, reps, tag):
     torch.cuda.empty_cache()
 
 
+def probe_reset_latency(N=65536):
+    """snake_reset over a mask of m envs out of N: latency of m concurrent resets."""
+    kw = dict(height=20, width=20, snake_length=3, vision_range=5)
+    v = SnakeVecEnv(N, num_snakes=4, seed=0, **kw)
+    v.reset()
+    out = {'tag': 'reset_mask', 'N': N}
+    for m in (1, 16, 256, 1024, 4096, N):
+        mask = torch.zeros(N, dtype=torch.bool, device='cuda')
+        mask[torch.randperm(N, device='cuda')[:m]] = True
+        out[f'm{m}'] = timed(lambda: v.reset(mask), 10)
+    print(json.dumps(out), flush=True)
+    small = SnakeVecEnv(64, num_snakes=4, seed=0, **kw)
+    small.reset()
+    g = torch.Generator(device='cuda').manual_seed(1)
+    acts = torch.randint(0, 3, (400, 64, 4), generator=g, device='cuda', dtype=torch.int8)
+    it = iter(range(10 ** 9))
+    print(json.dumps({'tag': 'step_auto_N64', **timed(lambda: small.step(acts[next(it) % 400]), 300)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=50)
     ap.add_argument('--quick', action='store_true')
+    ap.add_argument('--reset-latency', action='store_true')
     a = ap.parse_args()
+    if a.reset_latency:
+        probe_reset_latency()
+        return
     cfg3 = dict(height=20, width=20, snake_length=3, vision_range=5)
     for N in ((65536,) if a.quick else (4096, 16384, 65536, 262144)):
         probe(N, 4, cfg3, a.reps, 'cfg3')
