@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 2
+#define SNAKE_ABI_VERSION 3
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -63,6 +63,7 @@ typedef struct {
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
     int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
     int64_t jscratch;   /* uint16 [N][n_cand] reset scratch, 0 when it fits in LDS */
+    int64_t resetq;     /* int32  [N + 2]                auto-reset queue + two counters */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */
     int64_t rew;        /* double [N][S] */
     int64_t done;       /* uint8  [N][S] */
@@ -85,6 +86,7 @@ typedef struct {        /* device state buffers (layouts in snake_layout) */
     uint32_t *mt;
     const int16_t *cand;
     uint16_t *jscratch; /* may be NULL when layout.jscratch == 0 */
+    int32_t  *resetq;   /* zero-initialised once by the caller */
 } snake_state;
 
 typedef struct {        /* device output buffers of one step/reset */
@@ -118,7 +120,9 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
 
 /* SnakeEnv.step(actions) (snake_env.py:301-414) for all envs at once; actions is
  * int8 [N][S]. With cfg->autoreset an env whose dones are all True is reset in
- * the same launch and its out->obs holds the reset observation. */
+ * the same call and its out->obs holds the reset observation. Two launches: the
+ * game rules for every env, then the observations, whose first workgroups run
+ * the queued resets while the rest encode. */
 int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
                const int8_t *actions, const snake_out *out, void *stream);
 

@@ -196,10 +196,10 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->stats = N * 4 * S * 8;
     o->mt = N * kMtN * 4;
     o->cand = o->n_cand * c->snake_length * 2;
-    // Fisher-Yates draw record of a reset: global scratch, L2-resident while used.
-    // (Kept out of LDS so the step kernel's LDS, and with it its occupancy, stays
-    // at the grid ring + a few hundred bytes.)
-    o->jscratch = N * o->n_cand * 2;
+    // Fisher-Yates draw record of a reset: in LDS when small (the backward trace
+    // re-reads it), else global scratch.
+    o->jscratch = (o->n_cand * 2 <= kJarrLdsMax) ? 0 : N * o->n_cand * 2;
+    o->resetq = (N + 2) * 4;
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
     o->done = N * S;
@@ -250,7 +250,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->lds_frames = off; off += (int)round_up((int64_t)k->fs * k->grid_stride, 16);
     k->lds_centers = off; off += (int)round_up(4 * k->fs * kMaxSnakes, 16);
     k->lds_fruit = off; off += (int)round_up(2 * kMaxFruits, 16);
-    k->jarr_in_lds = 0;
+    k->jarr_in_lds = lay.jscratch == 0;
     k->lds_jarr = off;
     if (k->jarr_in_lds) off += (int)round_up(2 * (int64_t)k->n_cand, 16);
     k->lds_bytes = off;
@@ -268,6 +268,10 @@ static int check_state(const KCfg &k, const snake_state *st, bool need_all)
     if (!st || !st->grid || !st->snake || !st->body || !st->env || !st->ctr || !st->stats ||
         !st->mt || !st->cand) {
         set_error("snake_state has a NULL buffer");
+        return SNAKE_E_ARG;
+    }
+    if (!st->resetq) {
+        set_error("snake_state.resetq is NULL");
         return SNAKE_E_ARG;
     }
     if (!k.jarr_in_lds && !st->jscratch) {
@@ -359,7 +363,16 @@ int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, co
     if ((rc = check_state(k, st, true))) return rc;
     if ((rc = check_out(out, true))) return rc;
     if (!actions) { set_error("actions is NULL"); return SNAKE_E_ARG; }
-    return launch_step(k, *st, actions, *out, stream);
+    // The auto-reset queue has two counters used on alternate steps (each step's
+    // logic kernel zeroes the other one); the parity is per state, kept here.
+    static std::mutex mu;
+    static std::map<const void *, unsigned> ticks;
+    unsigned parity;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        parity = ticks[st->resetq]++ & 1u;
+    }
+    return launch_step(k, *st, actions, *out, (int)parity, stream);
 }
 
 }  // extern "C"

@@ -12,6 +12,7 @@ constexpr int kMtN = 624;
 constexpr int kMaxSnakes = 16;
 constexpr int kMaxFruits = 64;
 constexpr int kEnvRec = 8;          // int32 words per env record
+constexpr int kJarrLdsMax = 8192;   // bytes of reset draw record kept in LDS
 
 // env record words
 enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3 };
@@ -41,6 +42,6 @@ int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_
 int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, const snake_out &o,
                  void *stream);
 int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, const snake_out &o,
-                void *stream);
+                int parity, void *stream);
 
 }  // namespace snake

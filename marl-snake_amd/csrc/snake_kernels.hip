@@ -16,11 +16,41 @@
 // reference's order of operations (snake_env.py:365-369, :385-389).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "snake_internal.h"
+
+#ifndef SNAKE_STEP_MIN_WAVES
+#define SNAKE_STEP_MIN_WAVES 1   // waves per SIMD the step kernel is register-budgeted for
+#endif
 
 namespace snake {
 
+#ifdef SNAKE_STAMPS
+// Diagnostic build only: s_memtime stamps of env 0's wave at phase boundaries.
+__device__ unsigned long long g_stamps[64];
+__device__ unsigned long long g_counts[8];
+#define STAMP(e, lane, idx)                                                        \
+    do {                                                                           \
+        if ((e) == 0) {                                                            \
+            __builtin_amdgcn_sched_barrier(0);                                     \
+            unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
+            if ((lane) == 0) g_stamps[idx] = _t;                                   \
+            __builtin_amdgcn_sched_barrier(0);                                     \
+        }                                                                          \
+    } while (0)
+#define COUNT(e, lane, idx) do { if ((e) == 0 && (lane) == 0) g_counts[idx]++; } while (0)
+#else
+#define STAMP(e, lane, idx) do {} while (0)
+#define COUNT(e, lane, idx) do {} while (0)
+#endif
+
 enum { C_EMPTY = 0, C_WALL = 1, C_FRUIT = 2, C_HEAD = 3, C_BODY = 4, C_TAIL = 5 };
+
+// global-memory views (explicit address space: flat accesses would also count
+// against lgkmcnt and stall every LDS/cross-lane wait behind them)
+typedef __attribute__((address_space(1))) uint16_t gu16;
+typedef __attribute__((address_space(3))) uint16_t lu16;
 
 // Direction (core/snake.py:33-37): 0 UP(-1,0) 1 RIGHT(0,1) 2 DOWN(1,0) 3 LEFT(0,-1)
 __device__ __forceinline__ int dir_dr(int d) { return d == 0 ? -1 : (d == 2 ? 1 : 0); }
@@ -184,59 +214,66 @@ __device__ uint32_t mt_draw(WaveMT &m, uint32_t mask, uint32_t rng, int lane)
 }
 
 // permutation(n) = shuffle(arange(n)) draws j_i = random_interval(i) for
-// i = n-1 .. 1 (snake_env.py:581). Writes jarr[i] = j_i. A round covers the 64
-// raw words of one tempered register; lane l (offset d from the first unread
-// word) is a SURE reject when w > i, a SURE accept when w <= i - d (at most d
-// accepts precede it), else ambiguous: everything before the first ambiguous
-// lane is resolved at once with ballots, the ambiguous lane with the exact
-// accept count. Rounds never straddle a change of mask (i crossing 2^k).
-__device__ void mt_perm_draws(WaveMT &m, int n, uint16_t *jarr, int lane)
+// i = n-1 .. 1 (snake_env.py:581). Writes jarr[i] = j_i. A round covers the raw
+// words of one tempered register from the stream position on; lane l (offset d
+// from the first unread word) is a SURE accept when w <= i - d (at most d accepts
+// precede it), a reject when w > i, else ambiguous: everything before the first
+// ambiguous lane is resolved at once (accepts ranked by mbcnt), the ambiguous
+// lane with the exact accept count. Rounds never straddle a change of mask (i
+// crossing 2^k): the last lane of a round is capped at l0 + (i - lo).
+template <typename JP>
+__device__ void mt_perm_draws(WaveMT &m, int n, JP *jarr, int lane, int e = -1)
 {
     int i = n - 1;
+    if (i < 1) return;
+    uint32_t mask = gen_mask((uint32_t)i);
+    int lo = (int)(mask >> 1) + 1;
     int tc = -1;
     uint32_t tw = 0;
     while (i >= 1) {
-        if (m.pos >= kMtN) { mt_twist(m, lane); tc = -1; }
+        if (m.pos >= kMtN) { mt_twist(m, lane); tc = -1; COUNT(e, lane, 0); }
         const int t = m.pos >> 6, l0 = m.pos & 63;
         if (t != tc) { tw = temper(word_at(m, t)); tc = t; }
-        const uint32_t mask = gen_mask((uint32_t)i);
-        const int lo = (int)(mask >> 1) + 1;
-        const int e = (t << 6) + lane;
-        const int lim = l0 + (i - lo);
-        const bool valid = lane >= l0 && lane <= lim && e < kMtN;
-        const uint32_t w = tw & mask;
+        COUNT(e, lane, 1);
+        const int hi = min(min(63, kMtN - 1 - (t << 6)), l0 + (i - lo));
         const int d = lane - l0;
-        const bool rej = w > (uint32_t)i;
-        const bool sure = !rej && (int)w <= i - d;
-        const unsigned long long vm = __ballot(valid);
-        const unsigned long long am = __ballot(valid && !rej && !sure);
-        const unsigned long long sm = __ballot(valid && sure);
-        const int last = 63 - __clzll((long long)vm);
-        const int end = am ? (__ffsll((long long)am) - 1) : last + 1;
-        const unsigned long long below = end >= 64 ? ~0ull : ((1ull << end) - 1ull);
-        const unsigned long long acc = sm & below;
+        const bool valid = (unsigned)d <= (unsigned)(hi - l0);
+        const int w = (int)(tw & mask);
+        const bool sure = valid && w <= i - d;
+        const bool amb = valid && !sure && w <= i;
+        const unsigned long long am = __ballot(amb);
+        unsigned long long acc = __ballot(sure);
+        int end = hi + 1;
+        if (am) {
+            end = __ffsll((long long)am) - 1;
+            acc &= (1ull << end) - 1ull;
+        }
         if ((acc >> lane) & 1ull) {
-            const int rank = __popcll(acc & ((1ull << lane) - 1ull));
+            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(acc >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)acc, 0u));
             jarr[i - rank] = (uint16_t)w;
         }
         int A = __popcll(acc);
         if (am) {
-            const uint32_t wf = (uint32_t)bcast((int)w, end);
-            if ((int)wf <= i - A) {
+            const int wf = bcast(w, end);
+            if (wf <= i - A) {
                 if (lane == 0) jarr[i - A] = (uint16_t)wf;
                 A++;
             }
-            m.pos = (t << 6) + end + 1;
-        } else {
-            m.pos = (t << 6) + last + 1;
+            end++;
         }
+        m.pos = (t << 6) + end;
         i -= A;
+        if (i < lo && i >= 1) {
+            mask = gen_mask((uint32_t)i);
+            lo = (int)(mask >> 1) + 1;
+        }
     }
 }
 
 // Final arr[k] of the Fisher-Yates pass for k < S: walk each position
-// backwards through the swaps (i ascending = reverse of the draw order). Two
-// chunks of 64 swaps are read together; a pair that touches none of the S
+// backwards through the swaps (i ascending = reverse of the draw order). Four
+// chunks of 64 swaps are loaded together; a group that touches none of the S
 // tracked positions costs one ballot.
 template <int MS>
 __device__ __forceinline__ void trace_chunk(int b, int n, int jv, int S, int (&q)[MS], int lane)
@@ -257,22 +294,29 @@ __device__ __forceinline__ void trace_chunk(int b, int n, int jv, int S, int (&q
     }
 }
 
-template <int MS>
-__device__ void perm_trace(int n, const uint16_t *jarr, int S, int (&q)[MS], int lane)
+template <int MS, typename JP>
+__device__ void perm_trace(int n, const JP *jarr, int S, int (&q)[MS], int lane)
 {
 #pragma unroll
     for (int k = 0; k < MS; k++) q[k] = k;
-    for (int b0 = 1; b0 < n; b0 += 2 * kWave) {
-        const int i0 = b0 + lane, i1 = i0 + kWave;
+    for (int b0 = 1; b0 < n; b0 += 4 * kWave) {
+        const int i0 = b0 + lane, i1 = i0 + kWave, i2 = i1 + kWave, i3 = i2 + kWave;
         const int j0 = (i0 < n) ? (int)jarr[i0] : -1;
         const int j1 = (i1 < n) ? (int)jarr[i1] : -1;
+        const int j2 = (i2 < n) ? (int)jarr[i2] : -1;
+        const int j3 = (i3 < n) ? (int)jarr[i3] : -1;
         bool hit = false;
 #pragma unroll
-        for (int k = 0; k < MS; k++)
-            hit |= (k < S) && ((i0 < n && (i0 == q[k] || j0 == q[k])) || (i1 < n && (i1 == q[k] || j1 == q[k])));
+        for (int k = 0; k < MS; k++) {
+            if (k >= S) continue;
+            const int x = q[k];
+            hit |= (i0 == x || j0 == x || i1 == x || j1 == x || i2 == x || j2 == x || i3 == x || j3 == x);
+        }
         if (__ballot(hit) == 0ull) continue;
         trace_chunk<MS>(b0, n, j0, S, q, lane);
         trace_chunk<MS>(b0 + kWave, n, j1, S, q, lane);
+        trace_chunk<MS>(b0 + 2 * kWave, n, j2, S, q, lane);
+        trace_chunk<MS>(b0 + 3 * kWave, n, j3, S, q, lane);
     }
 }
 
@@ -392,15 +436,16 @@ __device__ __forceinline__ int dir_of_diff(int diff, int W)
 // permutation(n_cand)[:S] retried until disjoint (:576-589), Snake(idx, coords)
 // (core/snake.py:53-74), num_fruits fruit draws, first observation replicated
 // over the frame stack.
-template <int MS>
+template <int MS, bool JL>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
                          WaveMT &mt, uint8_t *lds, int lane)
 {
     uint8_t *frames = lds + c.lds_frames;
     int *org = reinterpret_cast<int *>(lds + c.lds_centers);
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
-    uint16_t *jarr = c.jarr_in_lds ? reinterpret_cast<uint16_t *>(lds + c.lds_jarr)
-                                   : st.jscratch + (int64_t)e * c.n_cand;
+    // the Fisher-Yates draw record: LDS when it fits the budget, else global scratch
+    typedef typename std::conditional<JL, lu16, gu16>::type JP;
+    JP *jarr = JL ? (JP *)(lds + c.lds_jarr) : (JP *)(st.jscratch + (int64_t)e * c.n_cand);
     uint8_t *work = frames + (c.fs - 1) * c.grid_stride;
     const int S = c.S, L = c.L, W = c.W, SL = S * L;
     const int sk = lane / L, si = lane - sk * L;
@@ -408,10 +453,13 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     // The reference retries forever; a board too crowded for S disjoint spawn
     // poses would hang the wave, so give up after 2^16 permutations.
     for (int attempt = 0; attempt < (1 << 16); attempt++) {
-        mt_perm_draws(mt, c.n_cand, jarr, lane);
-        if (c.jarr_in_lds) wave_sync(); else __syncthreads();
+        STAMP(e, lane, 1 + 3 * min(attempt, 3));
+        mt_perm_draws(mt, c.n_cand, jarr, lane, e);
+        STAMP(e, lane, 2 + 3 * min(attempt, 3));
+        if (JL) wave_sync(); else __syncthreads();   // the draw record, written by every lane
         int q[MS];
         perm_trace<MS>(c.n_cand, jarr, S, q, lane);
+        STAMP(e, lane, 3 + 3 * min(attempt, 3));
         int pk = 0;
 #pragma unroll
         for (int k = 0; k < MS; k++) pk = (sk == k) ? q[k] : pk;
@@ -421,7 +469,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
             const int cx = bcast(cell, x);
             dup |= (lane < SL && lane != x && cx == cell);
         }
-        if (c.jarr_in_lds) wave_sync(); else __syncthreads();
+        if (JL) wave_sync(); else __syncthreads();
         if (__ballot(dup) == 0ull) break;   // _clear_overlap (:568-574)
     }
     // make_grid (grid_util.py:14-20), then paint (:138-144)
@@ -455,7 +503,9 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         }
     }
     wave_sync();
+    STAMP(e, lane, 20);
     place_fruits(c, work, mt, c.num_fruits, fbuf, lane);        // :147-148
+    STAMP(e, lane, 21);
     uint8_t *gbase = st.grid + (int64_t)e * c.fs * c.grid_stride;
     const int n16 = c.grid_stride >> 4;
     for (int q = lane; q < n16; q += kWave) {
@@ -471,7 +521,9 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     if (lane < 4 * S) st.stats[(int64_t)e * 4 * S + lane] = 0.0;   // _reset_epi_stats
     mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
     wave_sync();
+    STAMP(e, lane, 22);
     encode(c, frames, org, 0, o.obs + (int64_t)e * c.units * 8, lane);
+    STAMP(e, lane, 23);
 }
 
 // -------------------------------------------------------------------- step
@@ -495,17 +547,22 @@ __device__ __forceinline__ void stage_to_lds(uint8_t *dst, const uint8_t *src, i
     }
 }
 
+// ---------------------------------------------------------- step: the rules
+// k_logic: one wave per env runs SnakeEnv.step up to the observation: rules,
+// grid update, fruit respawn, statistics and outputs; the new frame goes to its
+// ring slot; an env whose episode ended is queued for its auto-reset.
 template <int MS>
-__global__ void __launch_bounds__(64, 8) k_step(const KCfg c, const snake_state st,
-                                             const int8_t *__restrict__ actions, const snake_out o)
+__global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c, const snake_state st,
+                                                              const int8_t *__restrict__ actions,
+                                                              const snake_out o, int parity)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int e = blockIdx.x, lane = threadIdx.x;
     const int S = c.S, W = c.W, cap = c.ring_cap, fs = c.fs, stride = c.grid_stride;
-    uint8_t *frames = lds + c.lds_frames;                  // ring slots, slot order
-    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
-    uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
+    uint8_t *work = lds;                                   // the grid being stepped
+    uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + stride);
     const bool isn = lane < S;
+    if (e == 0 && lane == 0) st.resetq[c.N + (parity ^ 1)] = 0;   // next step's queue
 
     // ---- every load this step needs, issued up front (one memory round trip)
     const int4 er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
@@ -518,15 +575,8 @@ __global__ void __launch_bounds__(64, 8) k_step(const KCfg c, const snake_state 
         act = actions[(int64_t)e * S + lane];
         s0 = sp[lane]; s1 = sp[S + lane]; s2 = sp[2 * S + lane]; s3 = sp[3 * S + lane];
     }
-    stage_to_lds(frames, st.grid + (int64_t)e * c.ring_bytes, c.ring_bytes, lane);
-    if (fs > 1) {                             // crop centres of every ring slot
-        for (int q = lane; q < fs * S; q += kWave) {
-            const int x = q / S, k = q - x * S;
-            const int p = st.ctr[(int64_t)e * fs * S + q];
-            org[x * kMaxSnakes + k] = pack_origin(c, p >> 8, p & 255);
-        }
-    }
     const int alive0 = er.x, eplen = er.y, cur = er.z, mtpos = er.w;
+    stage_to_lds(work, st.grid + (int64_t)e * c.ring_bytes + cur * stride, stride, lane);
     const int ncur = (fs == 1) ? 0 : (cur + 1 == fs ? 0 : cur + 1);
     int hr = rec.x & 255, hc = (rec.x >> 8) & 255, tr = (rec.x >> 16) & 255, tc = (rec.x >> 24) & 255;
     int dir = rec.y & 3, alive = (rec.y >> 8) & 1;
@@ -544,18 +594,11 @@ __global__ void __launch_bounds__(64, 8) k_step(const KCfg c, const snake_state 
         nd = (act == 1) ? 3 : ((act == 2) ? 1 : dir);
     }
     if (__ballot(mv && c.observer == 0 && (act < 0 || act > 2))) {
-        if (lane == 0) o.err[e] = 1;       // action_angle_dict[action] KeyError: env untouched
+        if (lane == 0) { o.err[e] = 1; o.ep_done[e] = 0; }   // KeyError: env untouched
         return;
     }
     if (mv) dir = nd;
     const int ncell = mv ? (hr + dir_dr(dir)) * W + hc + dir_dc(dir) : -1 - lane;
-    // the new frame is built in the slot of the frame that leaves the stack
-    uint8_t *work = frames + ncur * stride;
-    if (fs > 1) {
-        wave_sync();
-        for (int q = lane; q < (stride >> 4); q += kWave)
-            reinterpret_cast<uint4 *>(work)[q] = reinterpret_cast<const uint4 *>(frames + cur * stride)[q];
-    }
     wave_sync();
 
     // _check_collision :521-544 -- groups of snakes with the same target cell
@@ -690,7 +733,14 @@ __global__ void __launch_bounds__(64, 8) k_step(const KCfg c, const snake_state 
         o.rew[(int64_t)e * S + lane] = rew;
         o.done[(int64_t)e * S + lane] = (uint8_t)fd;
     }
-    if (lane == 0) { o.ep_done[e] = ep_end ? 1 : 0; o.err[e] = 0; }
+    if (lane == 0) {
+        o.ep_done[e] = ep_end ? 1 : 0;
+        o.err[e] = 0;
+        if (ep_end && c.autoreset) {                  // queue the auto-reset
+            const int slot = atomicAdd(&st.resetq[c.N + parity], 1);
+            st.resetq[slot] = e;
+        }
+    }
     if (ep_end) {
         int rank = 1;
         for (int j = 0; j < S; j++) rank += (__shfl(s0, j) > s0);
@@ -703,34 +753,20 @@ __global__ void __launch_bounds__(64, 8) k_step(const KCfg c, const snake_state 
     }
     if (isn) { sp[lane] = s0; sp[S + lane] = s1; sp[2 * S + lane] = s2; sp[3 * S + lane] = s3; }
 
-    if (ep_end && c.autoreset) {   // vector-env auto-reset (wrappers.py:139-145)
-        if (!mt_loaded) mt_load(mt, st.mt + (int64_t)e * kMtN, mtpos, lane);
-        __builtin_amdgcn_s_setprio(3);      // a reset is ~100x a step: let it run ahead
-        do_reset<MS>(c, st, o, e, mt, lds, lane);
-        __builtin_amdgcn_s_setprio(0);
-        return;
-    }
-
-    // commit the new frame into its ring slot; records; crop centres
+    // commit the new frame into its ring slot; records; crop centre of the frame
     uint8_t *gdst = st.grid + (int64_t)e * c.ring_bytes + ncur * stride;
     for (int q = lane; q < (stride >> 4); q += kWave)
         reinterpret_cast<uint4 *>(gdst)[q] = reinterpret_cast<const uint4 *>(work)[q];
     // crop centre = the own HEAD cell: the new head while alive, (0,0) when dead
     const int chr = alive ? nhr : 0, chc = alive ? nhc : 0;
-    if (isn) {
-        org[ncur * kMaxSnakes + lane] = pack_origin(c, chr, chc);
-        if (fs > 1) st.ctr[((int64_t)e * fs + ncur) * S + lane] = (uint16_t)((chr << 8) | chc);
-    }
     if (lane == 0) {
         int4 ner;
         ner.x = alive_snakes; ner.y = eplen1; ner.z = ncur; ner.w = mt_loaded ? mt.pos : mtpos;
         *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = ner;
     }
     if (mt_loaded) mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
-    wave_sync();
-    encode(c, frames, org, fs == 1 ? 0 : (ncur + 1 == fs ? 0 : ncur + 1),
-           o.obs + (int64_t)e * c.units * 8, lane);
-    if (isn) {      // last: the ring read for ntdir had the whole encode to land
+    if (isn) {
+        st.ctr[((int64_t)e * fs + ncur) * S + lane] = (uint16_t)((chr << 8) | chc);
         int4 nrec;
         nrec.x = nhr | (nhc << 8) | (ntr << 16) | (ntc << 24);
         nrec.y = dir | (alive << 8);
@@ -740,6 +776,44 @@ __global__ void __launch_bounds__(64, 8) k_step(const KCfg c, const snake_state 
     }
 }
 
+// ---------------------------------------------------- step: the observation
+// k_obs: workgroups [0, nres) run the queued auto-resets (they start first and
+// overlap the encodes); workgroup nres + e encodes env e's stacked frames.
+template <int MS>
+__global__ void __launch_bounds__(64) k_obs(const KCfg c, const snake_state st, const snake_out o,
+                                            int parity, int nres)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    if ((int)blockIdx.x < nres) {
+        const int R = st.resetq[c.N + parity];
+        for (int idx = blockIdx.x; idx < R; idx += nres) {
+            const int e = st.resetq[idx];
+            WaveMT mt;
+            mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
+            __builtin_amdgcn_s_setprio(3);
+            if (c.jarr_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, lane);
+            else do_reset<MS, false>(c, st, o, e, mt, lds, lane);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        return;
+    }
+    const int e = blockIdx.x - nres;
+    if (c.autoreset && o.ep_done[e]) return;          // its reset writes the obs
+    const int fs = c.fs, S = c.S;
+    uint8_t *frames = lds + c.lds_frames;
+    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
+    const int cur = st.env[(int64_t)e * kEnvRec + ENV_CUR];
+    stage_to_lds(frames, st.grid + (int64_t)e * c.ring_bytes, c.ring_bytes, lane);
+    for (int q = lane; q < fs * S; q += kWave) {
+        const int x = q / S, k = q - x * S;
+        const int p = st.ctr[(int64_t)e * fs * S + q];
+        org[x * kMaxSnakes + k] = pack_origin(c, p >> 8, p & 255);
+    }
+    wave_sync();
+    encode(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lane);
+}
+
 template <int MS>
 __global__ void __launch_bounds__(64) k_reset(const KCfg c, const snake_state st,
                                               const uint8_t *__restrict__ mask, const snake_out o)
@@ -747,9 +821,11 @@ __global__ void __launch_bounds__(64) k_reset(const KCfg c, const snake_state st
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int e = blockIdx.x, lane = threadIdx.x;
     if (mask && !mask[e]) return;
+    STAMP(e, lane, 0);
     WaveMT mt;
     mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
-    do_reset<MS>(c, st, o, e, mt, lds, lane);
+    if (c.jarr_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, lane);
+    else do_reset<MS, false>(c, st, o, e, mt, lds, lane);
 }
 
 // np.random.seed(s): mt19937_seed (init_genrand), pos = 624.
@@ -797,13 +873,36 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
 }
 
 int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, const snake_out &o,
-                void *stream)
+                int parity, void *stream)
 {
-    const dim3 grid(k.N), block(kWave);
-    if (k.S <= 4) hipLaunchKernelGGL(k_step<4>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, actions, o);
-    else if (k.S <= 8) hipLaunchKernelGGL(k_step<8>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, actions, o);
-    else hipLaunchKernelGGL(k_step<16>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, actions, o);
-    return check_launch("k_step");
+    const hipStream_t sm = (hipStream_t)stream;
+    const int nres = k.autoreset ? (k.N < 2048 ? k.N : 2048) : 0;
+    const int lds_logic = k.grid_stride + 2 * kMaxFruits;
+    const dim3 g1(k.N), g2(nres + k.N), block(kWave);
+    if (k.S <= 4) {
+        hipLaunchKernelGGL(k_logic<4>, g1, block, lds_logic, sm, k, st, actions, o, parity);
+        hipLaunchKernelGGL(k_obs<4>, g2, block, k.lds_bytes, sm, k, st, o, parity, nres);
+    } else if (k.S <= 8) {
+        hipLaunchKernelGGL(k_logic<8>, g1, block, lds_logic, sm, k, st, actions, o, parity);
+        hipLaunchKernelGGL(k_obs<8>, g2, block, k.lds_bytes, sm, k, st, o, parity, nres);
+    } else {
+        hipLaunchKernelGGL(k_logic<16>, g1, block, lds_logic, sm, k, st, actions, o, parity);
+        hipLaunchKernelGGL(k_obs<16>, g2, block, k.lds_bytes, sm, k, st, o, parity, nres);
+    }
+    return check_launch("k_logic/k_obs");
 }
 
 }  // namespace snake
+
+#ifdef SNAKE_STAMPS
+extern "C" int snake_debug_stamps(unsigned long long *out /* 72 */)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_stamps), sizeof(unsigned long long) * 64) != hipSuccess)
+        return -1;
+    if (hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(snake::g_counts), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    unsigned long long z[8] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(snake::g_counts), z, sizeof z);
+    return 0;
+}
+#endif

@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 2
+SNAKE_ABI_VERSION = 3
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
@@ -30,7 +30,7 @@ class SnakeCfg(ctypes.Structure):
 
 class SnakeLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
-        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'obs', 'rew', 'done',
+        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'resetq', 'obs', 'rew', 'done',
         'ep_done', 'rank', 'ep_stats', 'err', 'n_cand')] + [
         ('obs_h', ctypes.c_int32), ('obs_w', ctypes.c_int32), ('obs_c', ctypes.c_int32),
         ('grid_stride', ctypes.c_int32), ('ring_cap', ctypes.c_int32)]
@@ -38,7 +38,7 @@ class SnakeLayout(ctypes.Structure):
 
 class SnakeState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
-        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch')]
+        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'resetq')]
 
 
 class SnakeOut(ctypes.Structure):
@@ -50,23 +50,24 @@ class NativeError(RuntimeError):
     pass
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    """Load libsnake_amd.so once; raise loudly when it is absent."""
-    global _lib
-    if _lib is not None:
-        return _lib
+def lib(path=None):
+    """Load libsnake_amd.so once; raise loudly when it is absent. `path` loads an
+    alternative build of the same ABI (A/B timing of kernel variants)."""
+    path = path or os.environ.get('SNAKE_LIB') or LIB_PATH
+    if path in _libs:
+        return _libs[path]
     # PyTorch owns device memory and streams: its HIP runtime must be the one in
     # the process before libsnake_amd.so resolves libamdhip64.so.7 (loading ours
     # first brings in /opt/rocm's copy beside torch's, and launches then fail
     # with "no ROCm-capable device").
     import torch  # noqa: F401
-    if not os.path.exists(LIB_PATH):
-        raise NativeError(f'{LIB_PATH} not built: run `python __graft_entry__.py` '
+    if not os.path.exists(path):
+        raise NativeError(f'{path} not built: run `python __graft_entry__.py` '
                           '(hipcc --offload-arch=gfx950); there is no CPU fallback')
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, I64 = ctypes.c_void_p, ctypes.c_int64
     L.snake_abi_version.restype = ctypes.c_int
     L.snake_last_error.restype = ctypes.c_char_p
@@ -81,13 +82,13 @@ def lib():
                              ctypes.POINTER(SnakeOut), P]
     if L.snake_abi_version() != SNAKE_ABI_VERSION:
         raise NativeError('libsnake_amd.so ABI version mismatch; rebuild it')
-    _lib = L
+    _libs[path] = L
     return L
 
 
-def check(rc):
+def check(rc, L=None):
     if rc < 0:
-        msg = lib().snake_last_error().decode(errors='replace')
+        msg = (L or lib()).snake_last_error().decode(errors='replace')
         if rc == -1:
             raise ValueError(msg)
         raise NativeError(f'snake C-ABI error {rc}: {msg}')

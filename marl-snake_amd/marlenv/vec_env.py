@@ -31,7 +31,7 @@ def _torch():
 
 class SnakeVecEnv:
     def __init__(self, num_envs, num_snakes=4, device=None, seed=0, env_offset=0,
-                 autoreset=True, coop=False, strict=False, **env_kwargs):
+                 autoreset=True, coop=False, strict=False, lib_path=None, **env_kwargs):
         torch = _torch()
         if not torch.cuda.is_available():
             raise RuntimeError('SnakeVecEnv needs a HIP device (MI355X); there is no CPU fallback')
@@ -43,7 +43,7 @@ class SnakeVecEnv:
         self.strict = bool(strict)
         self.seed_base = int(seed) & 0xffffffff
         self.env_offset = int(env_offset)
-        L = lib()
+        self._L = L = lib(lib_path)
         lay = SnakeLayout()
         check(L.snake_plan(ctypes.byref(self.cfg), N, ctypes.byref(lay)))
         self.layout = lay
@@ -66,6 +66,7 @@ class SnakeVecEnv:
         self.stats = buf(lay.stats, torch.float64)
         self.mt = buf(lay.mt, torch.int32)
         self.jscratch = buf(lay.jscratch, torch.int16) if lay.jscratch else None
+        self.resetq = buf(lay.resetq, torch.int32)
         cap = int(lay.n_cand) * self.cfg.snake_length
         host = np.zeros(cap, np.int16)
         n = check(L.snake_build_candidates(ctypes.byref(self.cfg), host.ctypes.data_as(ctypes.c_void_p), cap))
@@ -74,7 +75,8 @@ class SnakeVecEnv:
         self._state = SnakeState(
             self.grid.data_ptr(), self.snake.data_ptr(), self.body.data_ptr(), self.env_rec.data_ptr(),
             self.ctr.data_ptr(), self.stats.data_ptr(), self.mt.data_ptr(), self.cand.data_ptr(),
-            self.jscratch.data_ptr() if self.jscratch is not None else None)
+            self.jscratch.data_ptr() if self.jscratch is not None else None,
+            self.resetq.data_ptr())
         check(L.snake_seed(ctypes.byref(self.cfg), ctypes.byref(self._state), N, self.seed_base,
                            self.env_offset, self._stream()))
 
@@ -126,7 +128,7 @@ class SnakeVecEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.uint8).reshape(self.num_envs).contiguous()
-        check(lib().snake_reset(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+        check(self._L.snake_reset(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
                                 ctypes.c_void_p(m.data_ptr()) if m is not None else None,
                                 ctypes.byref(so), self._stream()))
         self._keep = m
@@ -147,7 +149,7 @@ class SnakeVecEnv:
             raise RuntimeError('call reset() before step()')
         a = self._actions(actions)
         out, so = self._new_out()
-        check(lib().snake_step(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+        check(self._L.snake_step(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
                                ctypes.c_void_p(a.data_ptr()), ctypes.byref(so), self._stream()))
         self._keep = a
         info = {'episode_done': out['ep_done'], 'rank': out['rank'],

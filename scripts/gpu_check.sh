@@ -26,6 +26,10 @@ for s in "$@"; do
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 50 --no-cpu-baseline ;;
         probe) step probe 600 python scripts/perf_probe.py ;;
         rlat) step rlat 300 python scripts/perf_probe.py --reset-latency ;;
+        stamps) step stamps 300 python scripts/reset_stamps.py marl-snake_amd/build/var/libsnake_stamps.so ;;
+        ab) step ab 600 python scripts/ab_probe.py marl-snake_amd/build/var/*.so ;;
+        ab2) step ab2 600 python scripts/ab_probe.py --cfg cfg2 --N 4096 marl-snake_amd/build/var/*.so ;;
+        ab5) step ab5 600 python scripts/ab_probe.py --cfg cfg5 --N 8192 marl-snake_amd/build/var/*.so ;;
         pmc) step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc1 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
              step pmc2 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc2 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
              step pmc3 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc3 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10

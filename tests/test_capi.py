@@ -49,7 +49,7 @@ def test_plan_sizes(native):
     assert native.lib().snake_plan(ctypes.byref(c), 65536, ctypes.byref(lay)) == 0
     assert (lay.obs_h, lay.obs_w, lay.obs_c) == (11, 11, 8)
     assert lay.obs == 65536 * 4 * 11 * 11 * 8
-    assert lay.n_cand == 3464 and lay.jscratch == 65536 * 3464 * 2
+    assert lay.n_cand == 3464 and lay.jscratch == 0
     assert lay.grid_stride == 400 and lay.ring_cap == 512
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
