@@ -39,10 +39,19 @@ __device__ unsigned long long g_counts[8];
             __builtin_amdgcn_sched_barrier(0);                                     \
         }                                                                          \
     } while (0)
-#define COUNT(e, lane, idx) do { if ((e) == 0 && (lane) == 0) g_counts[idx]++; } while (0)
+#define COUNT(e, lane, idx) do { cnt_[idx]++; } while (0)
+#define COUNT_DECL unsigned long long cnt_[4] = {0, 0, 0, 0}
+#define COUNT_ADD(idx, v) do { cnt_[idx] += (v); } while (0)
+#define COUNT_FLUSH(e, lane)                                                       \
+    do { if ((e) == 0 && (lane) == 0) { for (int q_ = 0; q_ < 4; q_++) g_counts[q_] += cnt_[q_]; } } while (0)
+#define NOW() __builtin_amdgcn_s_memtime()
 #else
 #define STAMP(e, lane, idx) do {} while (0)
 #define COUNT(e, lane, idx) do {} while (0)
+#define COUNT_DECL do {} while (0)
+#define COUNT_ADD(idx, v) do { (void)(v); } while (0)
+#define COUNT_FLUSH(e, lane) do {} while (0)
+#define NOW() 0ull
 #endif
 
 enum { C_EMPTY = 0, C_WALL = 1, C_FRUIT = 2, C_HEAD = 3, C_BODY = 4, C_TAIL = 5 };
@@ -213,62 +222,99 @@ __device__ uint32_t mt_draw(WaveMT &m, uint32_t mask, uint32_t rng, int lane)
     }
 }
 
+__device__ __forceinline__ int mbcnt64(unsigned long long x)
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(x >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)x, 0u));
+}
+
 // permutation(n) = shuffle(arange(n)) draws j_i = random_interval(i) for
-// i = n-1 .. 1 (snake_env.py:581). Writes jarr[i] = j_i. A round covers the raw
-// words of one tempered register from the stream position on; lane l (offset d
-// from the first unread word) is a SURE accept when w <= i - d (at most d accepts
-// precede it), a reject when w > i, else ambiguous: everything before the first
-// ambiguous lane is resolved at once (accepts ranked by mbcnt), the ambiguous
-// lane with the exact accept count. Rounds never straddle a change of mask (i
-// crossing 2^k): the last lane of a round is capped at l0 + (i - lo).
+// i = n-1 .. 1 (snake_env.py:581). Writes jarr[i] = j_i.
+// A round covers the unread raw words of one aligned register pair (2q, 2q+1):
+// lane l holds the words at stream offsets p = l - l0 (first register) and
+// 64 - l0 + l (second). A word is accepted iff (w & mask) <= i - A_p, A_p = the
+// accepts before it. The accept set is found by bound refinement: with acc (sure
+// accepts) and pos (possible accepts) every lane knows L = |acc before it| <= A_p
+// <= U = |pos before it|, and re-deciding every lane against both bounds fixes at
+// least the first undecided lane per pass (typically 1-2 passes). Words past the
+// accept that takes i below the current power-of-two bracket were judged with
+// the wrong mask: the round ends right after that accept.
 template <typename JP>
 __device__ void mt_perm_draws(WaveMT &m, int n, JP *jarr, int lane, int e = -1)
 {
     int i = n - 1;
     if (i < 1) return;
+    COUNT_DECL;
     uint32_t mask = gen_mask((uint32_t)i);
     int lo = (int)(mask >> 1) + 1;
-    int tc = -1;
-    uint32_t tw = 0;
+    int qc = -1;
+    uint32_t tw0 = 0, tw1 = 0;
     while (i >= 1) {
-        if (m.pos >= kMtN) { mt_twist(m, lane); tc = -1; COUNT(e, lane, 0); }
-        const int t = m.pos >> 6, l0 = m.pos & 63;
-        if (t != tc) { tw = temper(word_at(m, t)); tc = t; }
-        COUNT(e, lane, 1);
-        const int hi = min(min(63, kMtN - 1 - (t << 6)), l0 + (i - lo));
-        const int d = lane - l0;
-        const bool valid = (unsigned)d <= (unsigned)(hi - l0);
-        const int w = (int)(tw & mask);
-        const bool sure = valid && w <= i - d;
-        const bool amb = valid && !sure && w <= i;
-        const unsigned long long am = __ballot(amb);
-        unsigned long long acc = __ballot(sure);
-        int end = hi + 1;
-        if (am) {
-            end = __ffsll((long long)am) - 1;
-            acc &= (1ull << end) - 1ull;
+        if (m.pos >= kMtN) {
+            const unsigned long long t0_ = NOW();
+            mt_twist(m, lane);
+            qc = -1;
+            COUNT(e, lane, 0);
+            COUNT_ADD(2, NOW() - t0_);
         }
-        if ((acc >> lane) & 1ull) {
-            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(acc >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)acc, 0u));
-            jarr[i - rank] = (uint16_t)w;
-        }
-        int A = __popcll(acc);
-        if (am) {
-            const int wf = bcast(w, end);
-            if (wf <= i - A) {
-                if (lane == 0) jarr[i - A] = (uint16_t)wf;
-                A++;
+        const int q = m.pos >> 7, l0 = m.pos & 127;
+        if (q != qc) {
+            uint32_t a = 0, b = 0;
+#pragma unroll
+            for (int r = 0; r < 5; r++) {
+                const uint32_t sel = 0u - (uint32_t)(q == r);
+                a |= m.w[2 * r] & sel;
+                b |= m.w[2 * r + 1] & sel;
             }
-            end++;
+            tw0 = temper(a);
+            tw1 = temper(b);
+            qc = q;
         }
-        m.pos = (t << 6) + end;
+        COUNT(e, lane, 1);
+        const int base = q << 7;
+        const int p0 = lane - l0, p1 = 64 + lane - l0;
+        const bool v0 = p0 >= 0;
+        const bool v1 = p1 >= 0 && base + 64 + lane < kMtN;
+        const int w0 = (int)(tw0 & mask), w1 = (int)(tw1 & mask);
+        unsigned long long a0 = __ballot(v0 && w0 <= i - p0), a1 = __ballot(v1 && w1 <= i - p1);
+        unsigned long long c0 = __ballot(v0 && w0 <= i), c1 = __ballot(v1 && w1 <= i);
+        while ((a0 ^ c0) | (a1 ^ c1)) {
+            const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
+            const int L1 = __popcll(a0) + mbcnt64(a1), U1 = __popcll(c0) + mbcnt64(c1);
+            const unsigned long long na0 = __ballot(v0 && w0 <= i - U0);
+            const unsigned long long na1 = __ballot(v1 && w1 <= i - U1);
+            c0 = __ballot(v0 && w0 <= i - L0);
+            c1 = __ballot(v1 && w1 <= i - L1);
+            a0 = na0;
+            a1 = na1;
+        }
+        const int A0 = __popcll(a0);
+        int A = A0 + __popcll(a1);
+        int end = min(128, kMtN - base);
+        const int k = i - lo + 1;  // accepts left in this bracket
+        if (A >= k) {
+            if (A0 >= k) {
+                const int b = __ffsll((long long)__ballot(((a0 >> lane) & 1ull) && mbcnt64(a0) == k - 1)) - 1;
+                a0 &= (2ull << b) - 1ull;
+                a1 = 0;
+                end = b + 1;
+            } else {
+                const int k1 = k - A0;
+                const int b = __ffsll((long long)__ballot(((a1 >> lane) & 1ull) && mbcnt64(a1) == k1 - 1)) - 1;
+                a1 &= (2ull << b) - 1ull;
+                end = 64 + b + 1;
+            }
+            A = k;
+        }
+        if ((a0 >> lane) & 1ull) jarr[i - mbcnt64(a0)] = (uint16_t)w0;
+        if ((a1 >> lane) & 1ull) jarr[i - __popcll(a0) - mbcnt64(a1)] = (uint16_t)w1;
+        m.pos = base + end;
         i -= A;
         if (i < lo && i >= 1) {
             mask = gen_mask((uint32_t)i);
             lo = (int)(mask >> 1) + 1;
         }
     }
+    COUNT_FLUSH(e, lane);
 }
 
 // Final arr[k] of the Fisher-Yates pass for k < S: walk each position
@@ -295,8 +341,9 @@ __device__ __forceinline__ void trace_chunk(int b, int n, int jv, int S, int (&q
 }
 
 template <int MS, typename JP>
-__device__ void perm_trace(int n, const JP *jarr, int S, int (&q)[MS], int lane)
+__device__ void perm_trace(int n, const JP *jarr, int S, int (&q)[MS], int lane, int e = -1)
 {
+    COUNT_DECL;
 #pragma unroll
     for (int k = 0; k < MS; k++) q[k] = k;
     for (int b0 = 1; b0 < n; b0 += 4 * kWave) {
@@ -312,12 +359,15 @@ __device__ void perm_trace(int n, const JP *jarr, int S, int (&q)[MS], int lane)
             const int x = q[k];
             hit |= (i0 == x || j0 == x || i1 == x || j1 == x || i2 == x || j2 == x || i3 == x || j3 == x);
         }
+        COUNT_ADD(3, 1ull << 32);
         if (__ballot(hit) == 0ull) continue;
+        COUNT_ADD(3, 1);
         trace_chunk<MS>(b0, n, j0, S, q, lane);
         trace_chunk<MS>(b0 + kWave, n, j1, S, q, lane);
         trace_chunk<MS>(b0 + 2 * kWave, n, j2, S, q, lane);
         trace_chunk<MS>(b0 + 3 * kWave, n, j3, S, q, lane);
     }
+    COUNT_FLUSH(e, lane);
 }
 
 // ------------------------------------------------------------ fruit respawn
@@ -458,7 +508,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         STAMP(e, lane, 2 + 3 * min(attempt, 3));
         if (JL) wave_sync(); else __syncthreads();   // the draw record, written by every lane
         int q[MS];
-        perm_trace<MS>(c.n_cand, jarr, S, q, lane);
+        perm_trace<MS>(c.n_cand, jarr, S, q, lane, e);
         STAMP(e, lane, 3 + 3 * min(attempt, 3));
         int pk = 0;
 #pragma unroll

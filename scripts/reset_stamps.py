@@ -33,7 +33,8 @@ def run(v, mask):
     L.snake_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p))
     st = {names[i]: int(buf[i]) for i in sorted(names) if buf[i]}
     t0 = st['start']
-    return {'cycles': {k: x - t0 for k, x in st.items()}, 'twists': int(buf[64]), 'rounds': int(buf[65])}
+    return {'cycles': {k: x - t0 for k, x in st.items()}, 'twists': int(buf[64]), 'rounds': int(buf[65]),
+            'twist_cycles': int(buf[66]), 'trace_batches': int(buf[67]) >> 32, 'trace_hit_batches': int(buf[67]) & 0xffffffff}
 
 
 for N in (1, 65536):
