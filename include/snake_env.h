@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 3
+#define SNAKE_ABI_VERSION 4
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -62,7 +62,7 @@ typedef struct {
     int64_t stats;      /* double [N][4][S]              episode scores/steps/fruits/kills */
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
     int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
-    int64_t jscratch;   /* uint16 [N][n_cand] reset scratch, 0 when it fits in LDS */
+    int64_t jscratch;   /* uint32 [min(N,2048)][round4(n_cand)] reset link tables, 0 when in LDS */
     int64_t resetq;     /* int32  [N + 2]                auto-reset queue + two counters */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */
     int64_t rew;        /* double [N][S] */
@@ -85,7 +85,7 @@ typedef struct {        /* device state buffers (layouts in snake_layout) */
     double   *stats;
     uint32_t *mt;
     const int16_t *cand;
-    uint16_t *jscratch; /* may be NULL when layout.jscratch == 0 */
+    uint32_t *jscratch; /* may be NULL when layout.jscratch == 0 */
     int32_t  *resetq;   /* zero-initialised once by the caller */
 } snake_state;
 

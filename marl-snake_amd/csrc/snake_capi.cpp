@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -196,9 +197,10 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->stats = N * 4 * S * 8;
     o->mt = N * kMtN * 4;
     o->cand = o->n_cand * c->snake_length * 2;
-    // Fisher-Yates draw record of a reset: in LDS when small (the backward trace
-    // re-reads it), else global scratch.
-    o->jscratch = (o->n_cand * 2 <= kJarrLdsMax) ? 0 : N * o->n_cand * 2;
+    // Link tables of the resets in flight (snake_kernels.hip perm_trace): in LDS
+    // when small, else one global table per reset worker.
+    const int64_t link = round_up(o->n_cand, 4) * 4;
+    o->jscratch = (link <= kLinkLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     o->resetq = (N + 2) * 4;
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
@@ -250,9 +252,12 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->lds_frames = off; off += (int)round_up((int64_t)k->fs * k->grid_stride, 16);
     k->lds_centers = off; off += (int)round_up(4 * k->fs * kMaxSnakes, 16);
     k->lds_fruit = off; off += (int)round_up(2 * kMaxFruits, 16);
-    k->jarr_in_lds = lay.jscratch == 0;
-    k->lds_jarr = off;
-    if (k->jarr_in_lds) off += (int)round_up(2 * (int64_t)k->n_cand, 16);
+    k->link_stride = (int)round_up(k->n_cand, 4);
+    k->link_in_lds = 4 * k->link_stride <= kLinkLdsMax;
+    k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
+    k->lds_obs_bytes = off;
+    k->lds_link = off;
+    if (k->link_in_lds) off += 4 * k->link_stride;
     k->lds_bytes = off;
     if (k->lds_bytes > 64 * 1024) {
         set_error("grid ring of %d bytes per env does not fit the LDS budget", k->ring_bytes);
@@ -274,7 +279,7 @@ static int check_state(const KCfg &k, const snake_state *st, bool need_all)
         set_error("snake_state.resetq is NULL");
         return SNAKE_E_ARG;
     }
-    if (!k.jarr_in_lds && !st->jscratch) {
+    if (!k.link_in_lds && !st->jscratch) {
         set_error("snake_state.jscratch is required for this config (n_cand=%d)", k.n_cand);
         return SNAKE_E_ARG;
     }

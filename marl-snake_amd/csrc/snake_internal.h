@@ -12,7 +12,8 @@ constexpr int kMtN = 624;
 constexpr int kMaxSnakes = 16;
 constexpr int kMaxFruits = 64;
 constexpr int kEnvRec = 8;          // int32 words per env record
-constexpr int kJarrLdsMax = 8192;   // bytes of reset draw record kept in LDS
+constexpr int kLinkLdsMax = 16384;  // bytes of a reset link table kept in LDS
+constexpr int kResetSlots = 2048;   // concurrent reset workers (global link tables)
 
 // env record words
 enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3 };
@@ -28,7 +29,10 @@ struct KCfg {
     // step of 128 units expressed in the mixed radix (fs, ow, oh, S)
     int adv_f, adv_j, adv_i, adv_k;
     // dynamic LDS carve (bytes, 16-aligned)
-    int lds_frames, lds_centers, lds_fruit, lds_jarr, lds_bytes, jarr_in_lds;
+    int lds_frames, lds_centers, lds_fruit, lds_link, lds_bytes, link_in_lds;
+    int link_stride;            // round4(n_cand): u32 entries of one link table
+    int lds_obs_bytes;          // LDS of k_obs without reset workers: no link table
+    int reset_slots;            // min(N, kResetSlots)
     double rf, rk, rl, rw, rt, max_steps;
 };
 

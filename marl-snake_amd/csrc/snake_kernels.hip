@@ -30,6 +30,9 @@ namespace snake {
 // Diagnostic build only: s_memtime stamps of env 0's wave at phase boundaries.
 __device__ unsigned long long g_stamps[64];
 __device__ unsigned long long g_counts[8];
+__device__ unsigned long long g_obsprof[512];   // realtime (100 MHz) of k_obs resets / encodes
+#define OBSPROF(slot, lane)                                                          \
+    do { if ((lane) == 0) g_obsprof[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define STAMP(e, lane, idx)                                                        \
     do {                                                                           \
         if ((e) == 0) {                                                            \
@@ -40,10 +43,10 @@ __device__ unsigned long long g_counts[8];
         }                                                                          \
     } while (0)
 #define COUNT(e, lane, idx) do { cnt_[idx]++; } while (0)
-#define COUNT_DECL unsigned long long cnt_[4] = {0, 0, 0, 0}
+#define COUNT_DECL unsigned long long cnt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define COUNT_ADD(idx, v) do { cnt_[idx] += (v); } while (0)
 #define COUNT_FLUSH(e, lane)                                                       \
-    do { if ((e) == 0 && (lane) == 0) { for (int q_ = 0; q_ < 4; q_++) g_counts[q_] += cnt_[q_]; } } while (0)
+    do { if ((e) == 0 && (lane) == 0) { for (int q_ = 0; q_ < 8; q_++) g_counts[q_] += cnt_[q_]; } } while (0)
 #define NOW() __builtin_amdgcn_s_memtime()
 #else
 #define STAMP(e, lane, idx) do {} while (0)
@@ -52,14 +55,36 @@ __device__ unsigned long long g_counts[8];
 #define COUNT_ADD(idx, v) do { (void)(v); } while (0)
 #define COUNT_FLUSH(e, lane) do {} while (0)
 #define NOW() 0ull
+#define OBSPROF(slot, lane) do {} while (0)
 #endif
 
 enum { C_EMPTY = 0, C_WALL = 1, C_FRUIT = 2, C_HEAD = 3, C_BODY = 4, C_TAIL = 5 };
 
 // global-memory views (explicit address space: flat accesses would also count
 // against lgkmcnt and stall every LDS/cross-lane wait behind them)
-typedef __attribute__((address_space(1))) uint16_t gu16;
 typedef __attribute__((address_space(3))) uint16_t lu16;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(3))) uint32_t lu32;
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u32 gu4;
+typedef __attribute__((address_space(3))) v4u32 lu4;
+constexpr uint32_t kNoLink = 0xffffffffu;
+
+// Link-table access: LDS atomics are ds_min_u32, global ones L2 atomics; global
+// reads bypass the vector L1 (a previous attempt's chase may have cached lines).
+__device__ __forceinline__ void link_min(lu32 *p, uint32_t v)
+{
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void link_min(gu32 *p, uint32_t v)
+{
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t link_get(const lu32 *p) { return *p; }
+__device__ __forceinline__ uint32_t link_get(const gu32 *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Direction (core/snake.py:33-37): 0 UP(-1,0) 1 RIGHT(0,1) 2 DOWN(1,0) 3 LEFT(0,-1)
 __device__ __forceinline__ int dir_dr(int d) { return d == 0 ? -1 : (d == 2 ? 1 : 0); }
@@ -228,7 +253,9 @@ __device__ __forceinline__ int mbcnt64(unsigned long long x)
 }
 
 // permutation(n) = shuffle(arange(n)) draws j_i = random_interval(i) for
-// i = n-1 .. 1 (snake_env.py:581). Writes jarr[i] = j_i.
+// i = n-1 .. 1 (snake_env.py:581). Only arr[0..S) is ever used, so instead of the
+// draws themselves the pass records, for the backward trace (perm_trace):
+//   jsmall[i] = j_i for i < S, and link[x] = min{ i >= S : j_i = x < i }.
 // A round covers the unread raw words of one aligned register pair (2q, 2q+1):
 // lane l holds the words at stream offsets p = l - l0 (first register) and
 // 64 - l0 + l (second). A word is accepted iff (w & mask) <= i - A_p, A_p = the
@@ -238,8 +265,15 @@ __device__ __forceinline__ int mbcnt64(unsigned long long x)
 // least the first undecided lane per pass (typically 1-2 passes). Words past the
 // accept that takes i below the current power-of-two bracket were judged with
 // the wrong mask: the round ends right after that accept.
-template <typename JP>
-__device__ void mt_perm_draws(WaveMT &m, int n, JP *jarr, int lane, int e = -1)
+template <typename NP>
+__device__ __forceinline__ void perm_record(int ii, int w, int S, NP *link, lu16 *jsmall)
+{
+    if (ii < S) jsmall[ii] = (uint16_t)w;
+    else if (w != ii) link_min(link + w, (uint32_t)ii);
+}
+
+template <typename NP>
+__device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, lu16 *jsmall, int lane, int e = -1)
 {
     int i = n - 1;
     if (i < 1) return;
@@ -257,6 +291,7 @@ __device__ void mt_perm_draws(WaveMT &m, int n, JP *jarr, int lane, int e = -1)
             COUNT_ADD(2, NOW() - t0_);
         }
         const int q = m.pos >> 7, l0 = m.pos & 127;
+        const unsigned long long r0_ = NOW();
         if (q != qc) {
             uint32_t a = 0, b = 0;
 #pragma unroll
@@ -270,23 +305,33 @@ __device__ void mt_perm_draws(WaveMT &m, int n, JP *jarr, int lane, int e = -1)
             qc = q;
         }
         COUNT(e, lane, 1);
+        const unsigned long long r1_ = NOW();
+        COUNT_ADD(7, r1_ - r0_);
         const int base = q << 7;
         const int p0 = lane - l0, p1 = 64 + lane - l0;
-        const bool v0 = p0 >= 0;
-        const bool v1 = p1 >= 0 && base + 64 + lane < kMtN;
+        // valid lanes as uniform masks: ballots of bare compares stay v_cmp -> SGPR
+        const int n1 = min(64, kMtN - base - 64);
+        const unsigned long long vm0 = l0 < 64 ? (~0ull << l0) : 0ull;
+        const unsigned long long vm1 = (n1 == 64 ? ~0ull : ((1ull << n1) - 1ull)) &
+                                       (l0 > 64 ? (~0ull << (l0 - 64)) : ~0ull);
         const int w0 = (int)(tw0 & mask), w1 = (int)(tw1 & mask);
-        unsigned long long a0 = __ballot(v0 && w0 <= i - p0), a1 = __ballot(v1 && w1 <= i - p1);
-        unsigned long long c0 = __ballot(v0 && w0 <= i), c1 = __ballot(v1 && w1 <= i);
+        unsigned long long a0 = __ballot(w0 <= i - p0) & vm0, a1 = __ballot(w1 <= i - p1) & vm1;
+        unsigned long long c0 = __ballot(w0 <= i) & vm0, c1 = __ballot(w1 <= i) & vm1;
+        const unsigned long long r2_ = NOW();
+        COUNT_ADD(4, r2_ - r1_);
         while ((a0 ^ c0) | (a1 ^ c1)) {
+            COUNT_ADD(3, 1);
             const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
             const int L1 = __popcll(a0) + mbcnt64(a1), U1 = __popcll(c0) + mbcnt64(c1);
-            const unsigned long long na0 = __ballot(v0 && w0 <= i - U0);
-            const unsigned long long na1 = __ballot(v1 && w1 <= i - U1);
-            c0 = __ballot(v0 && w0 <= i - L0);
-            c1 = __ballot(v1 && w1 <= i - L1);
+            const unsigned long long na0 = __ballot(w0 <= i - U0) & vm0;
+            const unsigned long long na1 = __ballot(w1 <= i - U1) & vm1;
+            c0 = __ballot(w0 <= i - L0) & vm0;
+            c1 = __ballot(w1 <= i - L1) & vm1;
             a0 = na0;
             a1 = na1;
         }
+        const unsigned long long r3_ = NOW();
+        COUNT_ADD(5, r3_ - r2_);
         const int A0 = __popcll(a0);
         int A = A0 + __popcll(a1);
         int end = min(128, kMtN - base);
@@ -305,69 +350,41 @@ __device__ void mt_perm_draws(WaveMT &m, int n, JP *jarr, int lane, int e = -1)
             }
             A = k;
         }
-        if ((a0 >> lane) & 1ull) jarr[i - mbcnt64(a0)] = (uint16_t)w0;
-        if ((a1 >> lane) & 1ull) jarr[i - __popcll(a0) - mbcnt64(a1)] = (uint16_t)w1;
+        if ((a0 >> lane) & 1ull) perm_record(i - mbcnt64(a0), w0, S, link, jsmall);
+        if ((a1 >> lane) & 1ull) perm_record(i - __popcll(a0) - mbcnt64(a1), w1, S, link, jsmall);
         m.pos = base + end;
         i -= A;
         if (i < lo && i >= 1) {
             mask = gen_mask((uint32_t)i);
             lo = (int)(mask >> 1) + 1;
         }
+        COUNT_ADD(6, NOW() - r3_);
     }
     COUNT_FLUSH(e, lane);
 }
 
-// Final arr[k] of the Fisher-Yates pass for k < S: walk each position
-// backwards through the swaps (i ascending = reverse of the draw order). Four
-// chunks of 64 swaps are loaded together; a group that touches none of the S
-// tracked positions costs one ballot.
-template <int MS>
-__device__ __forceinline__ void trace_chunk(int b, int n, int jv, int S, int (&q)[MS], int lane)
+// Final arr[k] of the Fisher-Yates pass for k < S, lane k: walk position k
+// backwards through the swaps (i ascending). The swaps i < S only move positions
+// < S (j_i <= i): replay them from jsmall. After that the tracked position q < S
+// <= i is only moved by a swap with j_i = q, to position i; from position x the
+// next move is the first later swap with j = x: link[x]. Chains are ~ln(n) long.
+template <int MS, typename NP>
+__device__ void perm_trace(int S, const NP *link, const lu16 *jsmall, int (&q)[MS], int lane)
 {
-    const int i = b + lane;
-#pragma unroll
-    for (int k = 0; k < MS; k++) {
-        if (k >= S) continue;
-        int from = -1;
+    int x = lane;
+    for (int i = 1; i < S; i++) {
+        const int j = jsmall[i];
+        x = (x == i) ? j : (x == j ? i : x);
+    }
+    if (lane < S) {
         for (;;) {
-            const unsigned long long mk = __ballot(i < n && lane > from && (i == q[k] || jv == q[k]));
-            if (!mk) break;
-            const int f = __ffsll((long long)mk) - 1;
-            const int jf = bcast(jv, f);
-            q[k] = (b + f == q[k]) ? jf : b + f;
-            from = f;
+            const uint32_t y = link_get(link + x);
+            if (y == kNoLink) break;
+            x = (int)y;
         }
     }
-}
-
-template <int MS, typename JP>
-__device__ void perm_trace(int n, const JP *jarr, int S, int (&q)[MS], int lane, int e = -1)
-{
-    COUNT_DECL;
 #pragma unroll
-    for (int k = 0; k < MS; k++) q[k] = k;
-    for (int b0 = 1; b0 < n; b0 += 4 * kWave) {
-        const int i0 = b0 + lane, i1 = i0 + kWave, i2 = i1 + kWave, i3 = i2 + kWave;
-        const int j0 = (i0 < n) ? (int)jarr[i0] : -1;
-        const int j1 = (i1 < n) ? (int)jarr[i1] : -1;
-        const int j2 = (i2 < n) ? (int)jarr[i2] : -1;
-        const int j3 = (i3 < n) ? (int)jarr[i3] : -1;
-        bool hit = false;
-#pragma unroll
-        for (int k = 0; k < MS; k++) {
-            if (k >= S) continue;
-            const int x = q[k];
-            hit |= (i0 == x || j0 == x || i1 == x || j1 == x || i2 == x || j2 == x || i3 == x || j3 == x);
-        }
-        COUNT_ADD(3, 1ull << 32);
-        if (__ballot(hit) == 0ull) continue;
-        COUNT_ADD(3, 1);
-        trace_chunk<MS>(b0, n, j0, S, q, lane);
-        trace_chunk<MS>(b0 + kWave, n, j1, S, q, lane);
-        trace_chunk<MS>(b0 + 2 * kWave, n, j2, S, q, lane);
-        trace_chunk<MS>(b0 + 3 * kWave, n, j3, S, q, lane);
-    }
-    COUNT_FLUSH(e, lane);
+    for (int k = 0; k < MS; k++) q[k] = bcast(x, k);
 }
 
 // ------------------------------------------------------------ fruit respawn
@@ -488,14 +505,15 @@ __device__ __forceinline__ int dir_of_diff(int diff, int W)
 // over the frame stack.
 template <int MS, bool JL>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
-                         WaveMT &mt, uint8_t *lds, int lane)
+                         WaveMT &mt, uint8_t *lds, int slot, int lane)
 {
     uint8_t *frames = lds + c.lds_frames;
     int *org = reinterpret_cast<int *>(lds + c.lds_centers);
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
-    // the Fisher-Yates draw record: LDS when it fits the budget, else global scratch
-    typedef typename std::conditional<JL, lu16, gu16>::type JP;
-    JP *jarr = JL ? (JP *)(lds + c.lds_jarr) : (JP *)(st.jscratch + (int64_t)e * c.n_cand);
+    // the permutation's link table: LDS when it fits the budget, else global scratch
+    typedef typename std::conditional<JL, lu32, gu32>::type NP;
+    NP *link = JL ? (NP *)(lds + c.lds_link) : (NP *)(st.jscratch + (int64_t)slot * c.link_stride);
+    lu16 *jsmall = (lu16 *)(lds + c.lds_fruit);   // the fruit buffer is free until place_fruits
     uint8_t *work = frames + (c.fs - 1) * c.grid_stride;
     const int S = c.S, L = c.L, W = c.W, SL = S * L;
     const int sk = lane / L, si = lane - sk * L;
@@ -504,11 +522,14 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     // poses would hang the wave, so give up after 2^16 permutations.
     for (int attempt = 0; attempt < (1 << 16); attempt++) {
         STAMP(e, lane, 1 + 3 * min(attempt, 3));
-        mt_perm_draws(mt, c.n_cand, jarr, lane, e);
+        for (int x = 4 * lane; x < c.link_stride; x += 4 * kWave)
+            *(typename std::conditional<JL, lu4, gu4>::type *)(link + x) = (v4u32)kNoLink;
+        if (JL) wave_sync(); else __syncthreads();
+        mt_perm_draws(mt, c.n_cand, S, link, jsmall, lane, e);
         STAMP(e, lane, 2 + 3 * min(attempt, 3));
-        if (JL) wave_sync(); else __syncthreads();   // the draw record, written by every lane
+        if (JL) wave_sync(); else __syncthreads();   // the link table, written by every lane
         int q[MS];
-        perm_trace<MS>(c.n_cand, jarr, S, q, lane, e);
+        perm_trace<MS>(S, link, jsmall, q, lane);
         STAMP(e, lane, 3 + 3 * min(attempt, 3));
         int pk = 0;
 #pragma unroll
@@ -519,7 +540,6 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
             const int cx = bcast(cell, x);
             dup |= (lane < SL && lane != x && cx == cell);
         }
-        if (JL) wave_sync(); else __syncthreads();
         if (__ballot(dup) == 0ull) break;   // _clear_overlap (:568-574)
     }
     // make_grid (grid_util.py:14-20), then paint (:138-144)
@@ -842,13 +862,17 @@ __global__ void __launch_bounds__(64) k_obs(const KCfg c, const snake_state st, 
             WaveMT mt;
             mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
             __builtin_amdgcn_s_setprio(3);
-            if (c.jarr_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, lane);
-            else do_reset<MS, false>(c, st, o, e, mt, lds, lane);
+            if (idx < 128) OBSPROF(idx, lane);
+            if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, lane);
+            else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, lane);
+            if (idx < 128) OBSPROF(128 + idx, lane);
             __builtin_amdgcn_s_setprio(0);
         }
         return;
     }
     const int e = blockIdx.x - nres;
+    const bool prof_ = (e & 511) == 0 && (e >> 9) < 128;
+    if (prof_) OBSPROF(256 + (e >> 9), lane);
     if (c.autoreset && o.ep_done[e]) return;          // its reset writes the obs
     const int fs = c.fs, S = c.S;
     uint8_t *frames = lds + c.lds_frames;
@@ -862,6 +886,7 @@ __global__ void __launch_bounds__(64) k_obs(const KCfg c, const snake_state st, 
     }
     wave_sync();
     encode(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lane);
+    if (prof_) OBSPROF(384 + (e >> 9), lane);
 }
 
 template <int MS>
@@ -869,13 +894,17 @@ __global__ void __launch_bounds__(64) k_reset(const KCfg c, const snake_state st
                                               const uint8_t *__restrict__ mask, const snake_out o)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int e = blockIdx.x, lane = threadIdx.x;
-    if (mask && !mask[e]) return;
-    STAMP(e, lane, 0);
-    WaveMT mt;
-    mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
-    if (c.jarr_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, lane);
-    else do_reset<MS, false>(c, st, o, e, mt, lds, lane);
+    const int lane = threadIdx.x;
+    // one env per block with the link table in LDS, else reset_slots workers
+    // striding over the envs, each with its own global link table
+    for (int e = blockIdx.x; e < c.N; e += gridDim.x) {
+        if (mask && !mask[e]) continue;
+        STAMP(e, lane, 0);
+        WaveMT mt;
+        mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
+        if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, lane);
+        else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, lane);
+    }
 }
 
 // np.random.seed(s): mt19937_seed (init_genrand), pos = 624.
@@ -915,7 +944,7 @@ int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_
 int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, const snake_out &o,
                  void *stream)
 {
-    const dim3 grid(k.N), block(kWave);
+    const dim3 grid(k.link_in_lds ? k.N : k.reset_slots), block(kWave);
     if (k.S <= 4) hipLaunchKernelGGL(k_reset<4>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
     else if (k.S <= 8) hipLaunchKernelGGL(k_reset<8>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
     else hipLaunchKernelGGL(k_reset<16>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
@@ -926,18 +955,21 @@ int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, con
                 int parity, void *stream)
 {
     const hipStream_t sm = (hipStream_t)stream;
-    const int nres = k.autoreset ? (k.N < 2048 ? k.N : 2048) : 0;
+    const int nres = k.autoreset ? k.reset_slots : 0;
     const int lds_logic = k.grid_stride + 2 * kMaxFruits;
+    // the reset workers' link tables stay in LDS when they fit (global link
+    // tables cost far more in L2 atomics than the lower encode occupancy)
+    const int lds_obs = (nres && k.link_in_lds) ? k.lds_bytes : k.lds_obs_bytes;
     const dim3 g1(k.N), g2(nres + k.N), block(kWave);
     if (k.S <= 4) {
         hipLaunchKernelGGL(k_logic<4>, g1, block, lds_logic, sm, k, st, actions, o, parity);
-        hipLaunchKernelGGL(k_obs<4>, g2, block, k.lds_bytes, sm, k, st, o, parity, nres);
+        hipLaunchKernelGGL(k_obs<4>, g2, block, lds_obs, sm, k, st, o, parity, nres);
     } else if (k.S <= 8) {
         hipLaunchKernelGGL(k_logic<8>, g1, block, lds_logic, sm, k, st, actions, o, parity);
-        hipLaunchKernelGGL(k_obs<8>, g2, block, k.lds_bytes, sm, k, st, o, parity, nres);
+        hipLaunchKernelGGL(k_obs<8>, g2, block, lds_obs, sm, k, st, o, parity, nres);
     } else {
         hipLaunchKernelGGL(k_logic<16>, g1, block, lds_logic, sm, k, st, actions, o, parity);
-        hipLaunchKernelGGL(k_obs<16>, g2, block, k.lds_bytes, sm, k, st, o, parity, nres);
+        hipLaunchKernelGGL(k_obs<16>, g2, block, lds_obs, sm, k, st, o, parity, nres);
     }
     return check_launch("k_logic/k_obs");
 }
@@ -945,6 +977,15 @@ int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, con
 }  // namespace snake
 
 #ifdef SNAKE_STAMPS
+extern "C" int snake_debug_obsprof(unsigned long long *out /* 512 */)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_obsprof), sizeof(unsigned long long) * 512) != hipSuccess)
+        return -1;
+    unsigned long long z[512] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(snake::g_obsprof), z, sizeof z);
+    return 0;
+}
+
 extern "C" int snake_debug_stamps(unsigned long long *out /* 72 */)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_stamps), sizeof(unsigned long long) * 64) != hipSuccess)

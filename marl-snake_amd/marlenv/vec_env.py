@@ -65,7 +65,7 @@ class SnakeVecEnv:
         self.ctr = buf(lay.ctr, torch.int16)
         self.stats = buf(lay.stats, torch.float64)
         self.mt = buf(lay.mt, torch.int32)
-        self.jscratch = buf(lay.jscratch, torch.int16) if lay.jscratch else None
+        self.jscratch = buf(lay.jscratch, torch.int32) if lay.jscratch else None
         self.resetq = buf(lay.resetq, torch.int32)
         cap = int(lay.n_cand) * self.cfg.snake_length
         host = np.zeros(cap, np.int16)

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Timeline of one k_obs launch (diagnostic SNAKE_STAMPS build): s_memrealtime
+(100 MHz) at start/end of the first 128 queued resets and of every 512th
+env's encode block, relative to the earliest recorded start.
+
+    python scripts/obs_profile.py marl-snake_amd/build/libsnake_stamps.so
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, 'marl-snake_amd'), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from marlenv import SnakeVecEnv  # noqa: E402
+
+
+def main():
+    lib = os.path.abspath(sys.argv[1])
+    N = 65536
+    v = SnakeVecEnv(N, num_snakes=4, seed=0, lib_path=lib, height=20, width=20, snake_length=3, vision_range=5)
+    L = ctypes.CDLL(lib)
+    L.snake_debug_obsprof.argtypes = [ctypes.c_void_p]
+    buf = np.zeros(512, dtype=np.uint64)
+    g = torch.Generator(device='cuda').manual_seed(7)
+    acts = torch.randint(0, 3, (300, N, 4), generator=g, device='cuda', dtype=torch.int8)
+    v.reset()
+    for t in range(250):
+        v.step(acts[t])
+    torch.cuda.synchronize()
+    for t in range(250, 256):
+        L.snake_debug_obsprof(buf.ctypes.data_as(ctypes.c_void_p))
+        _, _, done, info = v.step(acts[t])
+        torch.cuda.synchronize()
+        nres = int(info['episode_done'].sum())
+        L.snake_debug_obsprof(buf.ctypes.data_as(ctypes.c_void_p))
+        b = buf.astype(np.int64)
+        rs, re_, es, ee = b[:128], b[128:256], b[256:384], b[384:512]
+        nr = min(nres, 128)
+        rs, re_ = rs[:nr], re_[:nr]
+        ok = ee > 0
+        t0 = min(rs.min() if nr else 1 << 62, es[es > 0].min())
+        us = lambda x: (x - t0) / 100.0   # noqa: E731
+        pct = lambda x: [round(float(np.percentile(x, p)), 1) for p in (0, 50, 90, 100)]  # noqa: E731
+        print(json.dumps({
+            'resets': nres,
+            'reset_start_us': pct(us(rs)) if nr else None,
+            'reset_dur_us': pct((re_ - rs) / 100.0) if nr else None,
+            'reset_end_us': pct(us(re_)) if nr else None,
+            'encode_start_us': pct(us(es[es > 0])),
+            'encode_end_us': pct(us(ee[ok])),
+            'encode_dur_us': pct((ee[ok] - es[ok]) / 100.0),
+        }), flush=True)
+
+
+if __name__ == '__main__':
+    main()

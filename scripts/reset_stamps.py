@@ -34,7 +34,8 @@ def run(v, mask):
     st = {names[i]: int(buf[i]) for i in sorted(names) if buf[i]}
     t0 = st['start']
     return {'cycles': {k: x - t0 for k, x in st.items()}, 'twists': int(buf[64]), 'rounds': int(buf[65]),
-            'twist_cycles': int(buf[66]), 'trace_batches': int(buf[67]) >> 32, 'trace_hit_batches': int(buf[67]) & 0xffffffff}
+            'twist_cycles': int(buf[66]), 'refine_iters': int(buf[67]), 'round_cycles': {
+                'select': int(buf[71]), 'setup': int(buf[68]), 'refine': int(buf[69]), 'epilogue': int(buf[70])}}
 
 
 for N in (1, 65536):
