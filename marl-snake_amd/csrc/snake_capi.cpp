@@ -199,7 +199,7 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->cand = o->n_cand * c->snake_length * 2;
     // Link tables of the resets in flight (snake_kernels.hip perm_trace): in LDS
     // when small, else one global table per reset worker.
-    const int64_t link = round_up(o->n_cand, 4) * 4;
+    const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
     o->jscratch = (link <= kLinkLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     o->resetq = (N + 2) * 4;
     o->obs = N * S * oh * ow * 8 * fs;
@@ -252,10 +252,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->lds_frames = off; off += (int)round_up((int64_t)k->fs * k->grid_stride, 16);
     k->lds_centers = off; off += (int)round_up(4 * k->fs * kMaxSnakes, 16);
     k->lds_fruit = off; off += (int)round_up(2 * kMaxFruits, 16);
-    k->link_stride = (int)round_up(k->n_cand, 4);
+    k->link_stride = (int)round_up(k->n_cand, 4) + kWave;
     k->link_in_lds = 4 * k->link_stride <= kLinkLdsMax;
     k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
     k->lds_obs_bytes = off;
+    k->lds_mtt = off; off += 4 * 640;
     k->lds_link = off;
     if (k->link_in_lds) off += 4 * k->link_stride;
     k->lds_bytes = off;

@@ -30,8 +30,9 @@ struct KCfg {
     int adv_f, adv_j, adv_i, adv_k;
     // dynamic LDS carve (bytes, 16-aligned)
     int lds_frames, lds_centers, lds_fruit, lds_link, lds_bytes, link_in_lds;
-    int link_stride;            // round4(n_cand): u32 entries of one link table
-    int lds_obs_bytes;          // LDS of k_obs without reset workers: no link table
+    int link_stride;            // round4(n_cand) + 64 per-lane dummies: u32 entries of a link table
+    int lds_mtt;                // tempered MT block (640 u32) of a reset worker
+    int lds_obs_bytes;          // LDS of k_encode: no reset worker state
     int reset_slots;            // min(N, kResetSlots)
     double rf, rk, rl, rw, rt, max_steps;
 };

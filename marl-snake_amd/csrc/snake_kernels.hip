@@ -16,7 +16,10 @@
 // reference's order of operations (snake_env.py:365-369, :385-389).
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "snake_internal.h"
 
@@ -30,7 +33,7 @@ namespace snake {
 // Diagnostic build only: s_memtime stamps of env 0's wave at phase boundaries.
 __device__ unsigned long long g_stamps[64];
 __device__ unsigned long long g_counts[8];
-__device__ unsigned long long g_obsprof[512];   // realtime (100 MHz) of k_obs resets / encodes
+__device__ unsigned long long g_obsprof[512];   // realtime (100 MHz) of auto-resets / encodes
 #define OBSPROF(slot, lane)                                                          \
     do { if ((lane) == 0) g_obsprof[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define STAMP(e, lane, idx)                                                        \
@@ -272,42 +275,58 @@ __device__ __forceinline__ void perm_record(int ii, int w, int S, NP *link, lu16
     else if (w != ii) link_min(link + w, (uint32_t)ii);
 }
 
+// The tempered key block, 640 words (the last 16 are never valid), in LDS: a
+// round reads its register pair with two ds_read_b32 instead of selecting it out
+// of the key registers.
+__device__ __forceinline__ void temper_block(const WaveMT &m, lu32 *mtt, int lane)
+{
+#pragma unroll
+    for (int t = 0; t < 10; t++) mtt[64 * t + lane] = temper(m.w[t]);
+}
+
 template <typename NP>
-__device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, lu16 *jsmall, int lane, int e = -1)
+__device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, lu32 *mtt,
+                              int lane, int e = -1)
 {
     int i = n - 1;
     if (i < 1) return;
     COUNT_DECL;
     uint32_t mask = gen_mask((uint32_t)i);
     int lo = (int)(mask >> 1) + 1;
-    int qc = -1;
-    uint32_t tw0 = 0, tw1 = 0;
+    // lanes with nothing to record write their own dummy entry past the table
+    NP *dummy = link + link_n + lane;
+    // the current register pair and the next one, read ahead so that the LDS
+    // atomics of a round are never waited for by the next round's reads
+    int qc = -2;   // -2: nothing read ahead
+    uint32_t tw0 = 0, tw1 = 0, nx0 = 0, nx1 = 0;
+    if (m.pos < kMtN) temper_block(m, mtt, lane);
     while (i >= 1) {
         if (m.pos >= kMtN) {
             const unsigned long long t0_ = NOW();
             mt_twist(m, lane);
-            qc = -1;
+            temper_block(m, mtt, lane);
+            qc = -2;
             COUNT(e, lane, 0);
             COUNT_ADD(2, NOW() - t0_);
         }
-        const int q = m.pos >> 7, l0 = m.pos & 127;
         const unsigned long long r0_ = NOW();
+        COUNT(e, lane, 1);
+        const int q = m.pos >> 7, l0 = m.pos & 127;
+        const int base = q << 7;
         if (q != qc) {
-            uint32_t a = 0, b = 0;
-#pragma unroll
-            for (int r = 0; r < 5; r++) {
-                const uint32_t sel = 0u - (uint32_t)(q == r);
-                a |= m.w[2 * r] & sel;
-                b |= m.w[2 * r + 1] & sel;
+            if (q == qc + 1) {
+                tw0 = nx0;
+                tw1 = nx1;
+            } else {
+                tw0 = mtt[base + lane];
+                tw1 = mtt[base + 64 + lane];
             }
-            tw0 = temper(a);
-            tw1 = temper(b);
+            if (q < 4) {
+                nx0 = mtt[base + 128 + lane];
+                nx1 = mtt[base + 192 + lane];
+            }
             qc = q;
         }
-        COUNT(e, lane, 1);
-        const unsigned long long r1_ = NOW();
-        COUNT_ADD(7, r1_ - r0_);
-        const int base = q << 7;
         const int p0 = lane - l0, p1 = 64 + lane - l0;
         // valid lanes as uniform masks: ballots of bare compares stay v_cmp -> SGPR
         const int n1 = min(64, kMtN - base - 64);
@@ -318,7 +337,7 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, lu16 *jsmall, i
         unsigned long long a0 = __ballot(w0 <= i - p0) & vm0, a1 = __ballot(w1 <= i - p1) & vm1;
         unsigned long long c0 = __ballot(w0 <= i) & vm0, c1 = __ballot(w1 <= i) & vm1;
         const unsigned long long r2_ = NOW();
-        COUNT_ADD(4, r2_ - r1_);
+        COUNT_ADD(4, r2_ - r0_);
         while ((a0 ^ c0) | (a1 ^ c1)) {
             COUNT_ADD(3, 1);
             const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
@@ -332,7 +351,7 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, lu16 *jsmall, i
         }
         const unsigned long long r3_ = NOW();
         COUNT_ADD(5, r3_ - r2_);
-        const int A0 = __popcll(a0);
+        int A0 = __popcll(a0);
         int A = A0 + __popcll(a1);
         int end = min(128, kMtN - base);
         const int k = i - lo + 1;  // accepts left in this bracket
@@ -341,6 +360,7 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, lu16 *jsmall, i
                 const int b = __ffsll((long long)__ballot(((a0 >> lane) & 1ull) && mbcnt64(a0) == k - 1)) - 1;
                 a0 &= (2ull << b) - 1ull;
                 a1 = 0;
+                A0 = k;
                 end = b + 1;
             } else {
                 const int k1 = k - A0;
@@ -350,8 +370,16 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, lu16 *jsmall, i
             }
             A = k;
         }
-        if ((a0 >> lane) & 1ull) perm_record(i - mbcnt64(a0), w0, S, link, jsmall);
-        if ((a1 >> lane) & 1ull) perm_record(i - __popcll(a0) - mbcnt64(a1), w1, S, link, jsmall);
+        const int ii0 = i - mbcnt64(a0), ii1 = i - A0 - mbcnt64(a1);
+        const bool r0 = (a0 >> lane) & 1ull, r1 = (a1 >> lane) & 1ull;
+        if (i - A + 1 >= S) {
+            // every index of the round >= S: unconditional ds_min, misses to the dummy
+            link_min((r0 && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
+            link_min((r1 && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
+        } else {
+            if (r0) perm_record(ii0, w0, S, link, jsmall);
+            if (r1) perm_record(ii1, w1, S, link, jsmall);
+        }
         m.pos = base + end;
         i -= A;
         if (i < lo && i >= 1) {
@@ -522,10 +550,10 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     // poses would hang the wave, so give up after 2^16 permutations.
     for (int attempt = 0; attempt < (1 << 16); attempt++) {
         STAMP(e, lane, 1 + 3 * min(attempt, 3));
-        for (int x = 4 * lane; x < c.link_stride; x += 4 * kWave)
+        for (int x = 4 * lane; x < c.link_stride - kWave; x += 4 * kWave)
             *(typename std::conditional<JL, lu4, gu4>::type *)(link + x) = (v4u32)kNoLink;
         if (JL) wave_sync(); else __syncthreads();
-        mt_perm_draws(mt, c.n_cand, S, link, jsmall, lane, e);
+        mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, (lu32 *)(lds + c.lds_mtt), lane, e);
         STAMP(e, lane, 2 + 3 * min(attempt, 3));
         if (JL) wave_sync(); else __syncthreads();   // the link table, written by every lane
         int q[MS];
@@ -847,30 +875,34 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
 }
 
 // ---------------------------------------------------- step: the observation
-// k_obs: workgroups [0, nres) run the queued auto-resets (they start first and
-// overlap the encodes); workgroup nres + e encodes env e's stacked frames.
+// Two kernels that run concurrently after k_logic (launch_step forks them onto
+// two streams): k_autoreset's workers run the queued auto-resets (latency-bound,
+// many registers, link table in LDS), k_encode encodes every other env's stacked
+// frames (bandwidth-bound, few registers: full occupancy).
 template <int MS>
-__global__ void __launch_bounds__(64) k_obs(const KCfg c, const snake_state st, const snake_out o,
-                                            int parity, int nres)
+__global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_state st, const snake_out o,
+                                                  int parity)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
-    if ((int)blockIdx.x < nres) {
-        const int R = st.resetq[c.N + parity];
-        for (int idx = blockIdx.x; idx < R; idx += nres) {
-            const int e = st.resetq[idx];
-            WaveMT mt;
-            mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
-            __builtin_amdgcn_s_setprio(3);
-            if (idx < 128) OBSPROF(idx, lane);
-            if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, lane);
-            else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, lane);
-            if (idx < 128) OBSPROF(128 + idx, lane);
-            __builtin_amdgcn_s_setprio(0);
-        }
-        return;
+    const int R = st.resetq[c.N + parity];
+    __builtin_amdgcn_s_setprio(3);
+    for (int idx = blockIdx.x; idx < R; idx += gridDim.x) {
+        const int e = st.resetq[idx];
+        WaveMT mt;
+        mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
+        if (idx < 128) OBSPROF(idx, lane);
+        if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, lane);
+        else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, lane);
+        if (idx < 128) OBSPROF(128 + idx, lane);
     }
-    const int e = blockIdx.x - nres;
+}
+
+__global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state st, const snake_out o)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    const int e = blockIdx.x;
     const bool prof_ = (e & 511) == 0 && (e >> 9) < 128;
     if (prof_) OBSPROF(256 + (e >> 9), lane);
     if (c.autoreset && o.ep_done[e]) return;          // its reset writes the obs
@@ -951,27 +983,72 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
     return check_launch("k_reset");
 }
 
+// A side stream and fork/join events per (device, caller stream): k_encode runs
+// on the side stream concurrently with k_autoreset on the caller's stream.
+struct SideCtx {
+    hipStream_t side;
+    hipEvent_t fork, join;
+};
+
+static int side_ctx(hipStream_t main, SideCtx *out)
+{
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, SideCtx> ctx;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        set_error("hipGetDevice failed");
+        return SNAKE_E_LAUNCH;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    auto it = ctx.find({dev, main});
+    if (it == ctx.end()) {
+        SideCtx c;
+        if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c.join, hipEventDisableTiming) != hipSuccess) {
+            set_error("side stream / event creation failed");
+            return SNAKE_E_LAUNCH;
+        }
+        it = ctx.emplace(std::make_pair(dev, main), c).first;
+    }
+    *out = it->second;
+    return SNAKE_OK;
+}
+
 int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, const snake_out &o,
                 int parity, void *stream)
 {
     const hipStream_t sm = (hipStream_t)stream;
-    const int nres = k.autoreset ? k.reset_slots : 0;
     const int lds_logic = k.grid_stride + 2 * kMaxFruits;
-    // the reset workers' link tables stay in LDS when they fit (global link
-    // tables cost far more in L2 atomics than the lower encode occupancy)
-    const int lds_obs = (nres && k.link_in_lds) ? k.lds_bytes : k.lds_obs_bytes;
-    const dim3 g1(k.N), g2(nres + k.N), block(kWave);
-    if (k.S <= 4) {
-        hipLaunchKernelGGL(k_logic<4>, g1, block, lds_logic, sm, k, st, actions, o, parity);
-        hipLaunchKernelGGL(k_obs<4>, g2, block, lds_obs, sm, k, st, o, parity, nres);
-    } else if (k.S <= 8) {
-        hipLaunchKernelGGL(k_logic<8>, g1, block, lds_logic, sm, k, st, actions, o, parity);
-        hipLaunchKernelGGL(k_obs<8>, g2, block, lds_obs, sm, k, st, o, parity, nres);
-    } else {
-        hipLaunchKernelGGL(k_logic<16>, g1, block, lds_logic, sm, k, st, actions, o, parity);
-        hipLaunchKernelGGL(k_obs<16>, g2, block, lds_obs, sm, k, st, o, parity, nres);
+    const dim3 g1(k.N), gr(k.reset_slots), block(kWave);
+    if (k.S <= 4) hipLaunchKernelGGL(k_logic<4>, g1, block, lds_logic, sm, k, st, actions, o, parity);
+    else if (k.S <= 8) hipLaunchKernelGGL(k_logic<8>, g1, block, lds_logic, sm, k, st, actions, o, parity);
+    else hipLaunchKernelGGL(k_logic<16>, g1, block, lds_logic, sm, k, st, actions, o, parity);
+    int rc = check_launch("k_logic");
+    if (rc) return rc;
+    if (!k.autoreset) {
+        hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
+        return check_launch("k_encode");
     }
-    return check_launch("k_logic/k_obs");
+    // fork: the resets go first on the caller's stream (dispatched the moment
+    // k_logic retires), the encodes follow on the side stream; join before return
+    SideCtx sc;
+    if ((rc = side_ctx(sm, &sc))) return rc;
+    if (hipEventRecord(sc.fork, sm) != hipSuccess || hipStreamWaitEvent(sc.side, sc.fork, 0) != hipSuccess) {
+        set_error("fork to the side stream failed");
+        return SNAKE_E_LAUNCH;
+    }
+    if (k.S <= 4) hipLaunchKernelGGL(k_autoreset<4>, gr, block, k.lds_bytes, sm, k, st, o, parity);
+    else if (k.S <= 8) hipLaunchKernelGGL(k_autoreset<8>, gr, block, k.lds_bytes, sm, k, st, o, parity);
+    else hipLaunchKernelGGL(k_autoreset<16>, gr, block, k.lds_bytes, sm, k, st, o, parity);
+    if ((rc = check_launch("k_autoreset"))) return rc;
+    hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sc.side, k, st, o);
+    if ((rc = check_launch("k_encode"))) return rc;
+    if (hipEventRecord(sc.join, sc.side) != hipSuccess || hipStreamWaitEvent(sm, sc.join, 0) != hipSuccess) {
+        set_error("join from the side stream failed");
+        return SNAKE_E_LAUNCH;
+    }
+    return SNAKE_OK;
 }
 
 }  // namespace snake

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Timeline of one k_obs launch (diagnostic SNAKE_STAMPS build): s_memrealtime
+"""Timeline of one step's observation phase (diagnostic SNAKE_STAMPS build): s_memrealtime
 (100 MHz) at start/end of the first 128 queued resets and of every 512th
 env's encode block, relative to the earliest recorded start.
 

@@ -54,7 +54,7 @@ def test_plan_sizes(native):
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
     assert lay.obs_c == 32 and lay.obs == 8192 * 8 * 11 * 11 * 32
-    assert lay.n_cand == 16424 and lay.jscratch == 2048 * 16424 * 4
+    assert lay.n_cand == 16424 and lay.jscratch == 2048 * (16424 + 64) * 4
     assert lay.grid == 8192 * 4 * 1600
 
 
