@@ -15,13 +15,23 @@ A step = one SnakeVecEnv.step() over the GPU's whole batch. The timed region is
 exactly K steps between barrier + synchronize on both sides; value = all envs of
 all ranks x K / the slowest rank's time.
 
+A step is three kernels (include/snake_env.h snake_step): k_logic (rules, all
+envs), then k_autoreset (the step's auto-resets) concurrently with k_encode (the
+observations of every other env, on the library's side stream).
+
 The JSON line also carries:
-  roofline     -- the step kernel's algorithmic HBM bytes (SURVEY.md 8(d):
-                  B = S*h*w*8*fs + (fs+1)*H*W + 10*S per env-step) / its average
-                  duration, timed with HIP events on the launch stream during the
-                  timed region, against the 8 TB/s HBM peak; `traffic` = HBM bytes
-                  per launch from rocprofv3 PMC counters when profiles/pmc_traffic.json
-                  holds a measurement for this workload, else null.
+  roofline     -- k_encode, the kernel that moves the bulk of SURVEY.md 8(d)'s
+                  bytes: per launch (N - resets) x (S*h*w*8*fs obs write + fs*H*W
+                  frame reads) / its average duration, timed by the library's HIP
+                  timing events on k_encode's own stream during the timed region
+                  (snake_timing_enable; every --timing-stride-th step, default 8),
+                  against the 8 TB/s HBM peak; `traffic` =
+                  HBM bytes per k_encode launch from rocprofv3 PMC counters when
+                  profiles/pmc_traffic.json holds a measurement for this workload.
+  step_roofline -- the whole step against the same peak: B = S*h*w*8*fs +
+                  (fs+1)*H*W + 10*S bytes per env-step x envs /
+                  ms_per_step.
+  kernels      -- average device ms per launch of each step kernel (same events).
   cpu_baseline -- rank 0 at N=1: the CPU restatement (oracle/, a C port of the
                   reference SnakeEnv, 1 core) timed on a bounded sample of the same
                   workload on this host.
@@ -48,9 +58,25 @@ def shard_range(n_total, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def reduce_max(values, device, dist=None):
+    """Element-wise max over ranks (the slowest rank's times); identity at world 1."""
+    if dist is None:
+        return list(values)
+    import torch
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
 def algorithmic_bytes(S, h, w, fs, H, W):
     """obs write + grid ring read/write + actions/rewards/dones."""
     return S * h * w * 8 * fs + (fs + 1) * H * W + S * (1 + 8 + 1)
+
+
+def encode_bytes(S, h, w, fs, H, W):
+    """k_encode per encoded env: the stacked-frame observation written + the fs
+    grid frames read."""
+    return S * h * w * 8 * fs + fs * H * W
 
 
 def cpu_baseline(env_kw, num_snakes, seconds):
@@ -81,7 +107,7 @@ def cpu_baseline(env_kw, num_snakes, seconds):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=500)
+    ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=200)
     ap.add_argument('--envs-per-gpu', type=int, default=65536)
     ap.add_argument('--height', type=int, default=20)
@@ -91,6 +117,9 @@ def main():
     ap.add_argument('--frame-stack', type=int, default=1)
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--timing-stride', type=int, default=8,
+                    help='bracket the kernels of every k-th timed step with timing events '
+                         '(0: none; the events cost ~12 us per timed step)')
     args = ap.parse_args()
 
     import torch
@@ -110,6 +139,7 @@ def main():
     device = torch.device('cuda', local_rank if distributed else torch.cuda.current_device())
 
     from marlenv import SnakeVecEnv
+    from marlenv import _native
 
     per = args.envs_per_gpu
     n_total = per * world
@@ -128,38 +158,43 @@ def main():
         venv.step(actions[t])
     torch.cuda.synchronize(device)
 
-    stream = torch.cuda.current_stream(device)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    episodes = torch.zeros((), dtype=torch.int64, device=device)
+    L = _native.lib()
+    for k in ('k_logic', 'k_autoreset', 'k_encode', 'resets'):
+        _native.timing_read(k, L)                      # drop anything from the warmup
+    stride = args.timing_stride
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for t in range(args.steps):
-        ev[t][0].record(stream)
-        _, _, _, info = venv.step(actions[args.warmup + t])
-        ev[t][1].record(stream)
+        timed = stride > 0 and t % stride == 0
+        if timed:
+            _native.timing_enable(True, L)
+        venv.step(actions[args.warmup + t])
+        if timed:
+            _native.timing_enable(False, L)
     torch.cuda.synchronize(device)
     if distributed:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    episodes += info['episode_done'].sum()
+    kern = {}
+    for k in ('k_logic', 'k_autoreset', 'k_encode'):
+        ms, n = _native.timing_read(k, L)
+        kern[k] = ms / max(n, 1)
+    resets = _native.timing_read('resets', L)[1]
 
-    if distributed:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        km = torch.tensor([kern_ms], dtype=torch.float64, device=device)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kern_ms = float(km.item())
+    red = reduce_max([elapsed] + list(kern.values()), device, dist if distributed else None)
+    elapsed, kern = red[0], dict(zip(kern, red[1:]))
 
     lay = venv.layout
     B = algorithmic_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
-    achieved = B * (hi - lo) / (kern_ms * 1e-3) / 1e9
+    Be = encode_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
+    encoded_per_launch = (hi - lo) - resets / args.steps
+    enc_ms = kern['k_encode']
+    achieved = Be * encoded_per_launch / (enc_ms * 1e-3) / 1e9 if enc_ms > 0 else float('nan')
     value = n_total * args.steps / elapsed
+    step_gbs = B * (hi - lo) / (elapsed / args.steps) / 1e9
     workload = (f'cfg3: {per} envs/GPU x (20x20, 4 snakes, vision_range=5, frame_stack=1), '
                 'random actions, all-done auto-reset in the step'
                 if (args.height, args.width, S, args.vision_range, args.frame_stack) == (20, 20, 4, 5, 1)
@@ -170,7 +205,7 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            key = f'{args.height}x{args.width}_S{S}_vr{args.vision_range}_fs{args.frame_stack}_N{hi - lo}'
+            key = f'k_encode_{args.height}x{args.width}_S{S}_vr{args.vision_range}_fs{args.frame_stack}_N{hi - lo}'
             if key in pm:
                 traffic = pm[key]['hbm_bytes_per_launch']
         except (OSError, ValueError, KeyError):
@@ -194,8 +229,13 @@ def main():
                    'snake_length': 3, 'parallelism': f'env-shard x{world}'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                     'traffic': traffic, 'algorithmic_bytes_per_env_step': B,
-                     'kernel_ms': round(kern_ms, 4)},
+                     'traffic': traffic, 'kernel': 'k_encode', 'kernel_ms': round(enc_ms, 4),
+                     'algorithmic_bytes_per_launch': round(Be * encoded_per_launch),
+                     'bytes_per_encoded_env': Be},
+        'step_roofline': {'achieved': round(step_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                          'frac': round(step_gbs / HBM_PEAK_GBS, 4), 'bytes_per_env_step': B},
+        'kernels': {k: round(v, 4) for k, v in kern.items()},
+        'resets_per_step': round(resets / args.steps, 1),
         'cpu_baseline': None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 4
+#define SNAKE_ABI_VERSION 5
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -120,11 +120,20 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
 
 /* SnakeEnv.step(actions) (snake_env.py:301-414) for all envs at once; actions is
  * int8 [N][S]. With cfg->autoreset an env whose dones are all True is reset in
- * the same call and its out->obs holds the reset observation. Two launches: the
- * game rules for every env, then the observations, whose first workgroups run
- * the queued resets while the rest encode. */
+ * the same call and its out->obs holds the reset observation. Launches: k_logic
+ * (the game rules of every env, queueing the auto-resets), then k_autoreset on
+ * `stream` concurrently with k_encode (every other env's observation) on a side
+ * stream the library keeps per caller stream; joined before the call returns. */
 int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
                const int8_t *actions, const snake_out *out, void *stream);
+
+/* Profiling aid. While enabled, every kernel launch of snake_step / snake_reset
+ * is bracketed by timing events on its own stream. snake_timing_read returns the
+ * summed device time (ms) and the launch count of one kernel ("k_logic",
+ * "k_autoreset", "k_encode", "k_reset") since its last read, and the number of
+ * auto-resets run (kernel "resets": count only); it waits for the events. */
+int snake_timing_enable(int on);
+int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
 
 /* Last error message of this thread ("" if none). */
 const char *snake_last_error(void);

@@ -1,22 +1,28 @@
 // snake_kernels.hip -- the batched multi-snake env step on CDNA4 (gfx950).
 //
-// One 64-lane wavefront (= one workgroup) per env instance:
-//   * the env's grid ring (fs uint8 H x W frames) is staged in LDS with 16-byte loads;
-//   * the game rules (snake_env.py:301-374) run lane-parallel, lane k = snake k:
-//     targets, collision groups (readlane broadcasts), the fruit-eater tail
-//     rule, rewards, and a two-phase grid update (all tail clears, then all
-//     BODY/HEAD/TAIL writes) that reproduces the reference's snake-order update
-//     exactly ("two-phase update");
-//   * the wave-parallel parts use all 64 lanes: dead-body erase (prefix-scanned
-//     direction deque), fruit respawn (lane-chunked empty-cell ranking + MT19937
-//     rejection sampling resolved by ballots), the NHWC one-hot observation
-//     encode (16-byte coalesced stores), and the auto-reset (in-register MT19937
-//     twist, ballot-resolved Fisher-Yates draws, backward permutation trace).
+// One 64-lane wavefront (= one workgroup) per env instance or per reset worker.
+// snake_step = k_logic, then k_autoreset concurrently with k_encode:
+//   * k_logic: the env's current grid staged in LDS with 16-byte loads; the game
+//     rules (snake_env.py:301-374) lane-parallel, lane k = snake k: targets,
+//     collision groups (readlane broadcasts), the fruit-eater tail rule, rewards,
+//     and a two-phase grid update (all tail clears, then all BODY/HEAD/TAIL
+//     writes) that reproduces the reference's snake-order update exactly
+//     ("two-phase update"); dead-body erase (prefix-scanned direction
+//     deque), fruit respawn (lane-chunked empty-cell ranking + MT19937 rejection
+//     sampling resolved by ballots); envs whose dones are all True are queued;
+//   * k_encode: the NHWC one-hot observation from the grid ring, 16-byte stores;
+//   * k_autoreset / k_reset: in-register MT19937 twist, Fisher-Yates draws in
+//     ballot-refined rounds recording a link table, pointer-chase trace of
+//     arr[:S], paint, fruits, encode.
 // Compiled with -ffp-contract=off: rewards/statistics are float64 in the
 // reference's order of operations (snake_env.py:365-369, :385-389).
 #include <hip/hip_runtime.h>
 
+#include <string.h>
+
 #include <map>
+#include <string>
+#include <vector>
 #include <mutex>
 #include <type_traits>
 #include <utility>
@@ -28,6 +34,8 @@
 #endif
 
 namespace snake {
+
+__device__ unsigned long long g_resets_run;   // auto-resets run (snake_timing_read "resets")
 
 #ifdef SNAKE_STAMPS
 // Diagnostic build only: s_memtime stamps of env 0's wave at phase boundaries.
@@ -886,6 +894,7 @@ __global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_stat
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
     const int R = st.resetq[c.N + parity];
+    if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
     __builtin_amdgcn_s_setprio(3);
     for (int idx = blockIdx.x; idx < R; idx += gridDim.x) {
         const int e = st.resetq[idx];
@@ -953,6 +962,62 @@ __global__ void k_seed(const KCfg c, const snake_state st, uint32_t base, long l
     st.env[(int64_t)e * kEnvRec + ENV_MTPOS] = kMtN;
 }
 
+// ------------------------------------------------------------- kernel timing
+// Profiling aid (snake_timing_enable / snake_timing_read): pairs of timing events
+// around each launch, resolved when read. Event objects are pooled.
+namespace {
+struct TimingRec {
+    const char *name;
+    hipEvent_t a, b;
+};
+std::mutex g_tmu;
+bool g_timing = false;
+std::vector<TimingRec> g_pending;
+std::vector<hipEvent_t> g_pool;
+std::map<std::string, std::pair<double, int64_t>> g_done;
+
+hipEvent_t pooled_event()
+{
+    if (!g_pool.empty()) {
+        hipEvent_t ev = g_pool.back();
+        g_pool.pop_back();
+        return ev;
+    }
+    hipEvent_t ev = nullptr;
+    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    return ev;
+}
+}  // namespace
+
+// Brackets one launch: open() before it, close() after it (no-ops when off).
+struct TimedLaunch {
+    const char *name;
+    hipStream_t s;
+    hipEvent_t a = nullptr;
+    TimedLaunch(const char *n, hipStream_t st) : name(n), s(st)
+    {
+        std::lock_guard<std::mutex> g(g_tmu);
+        if (!g_timing) return;
+        a = pooled_event();
+        if (a && hipEventRecord(a, s) != hipSuccess) {
+            g_pool.push_back(a);
+            a = nullptr;
+        }
+    }
+    void close()
+    {
+        if (!a) return;
+        std::lock_guard<std::mutex> g(g_tmu);
+        hipEvent_t b = pooled_event();
+        if (b && hipEventRecord(b, s) == hipSuccess) {
+            g_pending.push_back({name, a, b});
+        } else {
+            g_pool.push_back(a);
+            if (b) g_pool.push_back(b);
+        }
+    }
+};
+
 // ---------------------------------------------------------------- launchers
 static int check_launch(const char *what)
 {
@@ -977,9 +1042,11 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
                  void *stream)
 {
     const dim3 grid(k.link_in_lds ? k.N : k.reset_slots), block(kWave);
+    TimedLaunch tl("k_reset", (hipStream_t)stream);
     if (k.S <= 4) hipLaunchKernelGGL(k_reset<4>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
     else if (k.S <= 8) hipLaunchKernelGGL(k_reset<8>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
     else hipLaunchKernelGGL(k_reset<16>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
+    tl.close();
     return check_launch("k_reset");
 }
 
@@ -1021,13 +1088,17 @@ int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, con
     const hipStream_t sm = (hipStream_t)stream;
     const int lds_logic = k.grid_stride + 2 * kMaxFruits;
     const dim3 g1(k.N), gr(k.reset_slots), block(kWave);
+    TimedLaunch t1("k_logic", sm);
     if (k.S <= 4) hipLaunchKernelGGL(k_logic<4>, g1, block, lds_logic, sm, k, st, actions, o, parity);
     else if (k.S <= 8) hipLaunchKernelGGL(k_logic<8>, g1, block, lds_logic, sm, k, st, actions, o, parity);
     else hipLaunchKernelGGL(k_logic<16>, g1, block, lds_logic, sm, k, st, actions, o, parity);
+    t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;
     if (!k.autoreset) {
+        TimedLaunch t3("k_encode", sm);
         hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
+        t3.close();
         return check_launch("k_encode");
     }
     // fork: the resets go first on the caller's stream (dispatched the moment
@@ -1038,11 +1109,15 @@ int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, con
         set_error("fork to the side stream failed");
         return SNAKE_E_LAUNCH;
     }
+    TimedLaunch t2("k_autoreset", sm);
     if (k.S <= 4) hipLaunchKernelGGL(k_autoreset<4>, gr, block, k.lds_bytes, sm, k, st, o, parity);
     else if (k.S <= 8) hipLaunchKernelGGL(k_autoreset<8>, gr, block, k.lds_bytes, sm, k, st, o, parity);
     else hipLaunchKernelGGL(k_autoreset<16>, gr, block, k.lds_bytes, sm, k, st, o, parity);
+    t2.close();
     if ((rc = check_launch("k_autoreset"))) return rc;
+    TimedLaunch t3("k_encode", sc.side);
     hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sc.side, k, st, o);
+    t3.close();
     if ((rc = check_launch("k_encode"))) return rc;
     if (hipEventRecord(sc.join, sc.side) != hipSuccess || hipStreamWaitEvent(sm, sc.join, 0) != hipSuccess) {
         set_error("join from the side stream failed");
@@ -1052,6 +1127,51 @@ int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, con
 }
 
 }  // namespace snake
+
+extern "C" int snake_timing_enable(int on)
+{
+    std::lock_guard<std::mutex> g(snake::g_tmu);
+    snake::g_timing = on != 0;
+    return SNAKE_OK;
+}
+
+extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *count)
+{
+    if (!kernel || !total_ms || !count) {
+        snake::set_error("snake_timing_read: NULL argument");
+        return SNAKE_E_ARG;
+    }
+    if (!strcmp(kernel, "resets")) {
+        unsigned long long n = 0, z = 0;
+        if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(snake::g_resets_run), sizeof n) != hipSuccess ||
+            hipMemcpyToSymbol(HIP_SYMBOL(snake::g_resets_run), &z, sizeof z) != hipSuccess) {
+            snake::set_error("snake_timing_read: reading the reset counter failed");
+            return SNAKE_E_LAUNCH;
+        }
+        *total_ms = 0.0;
+        *count = (int64_t)n;
+        return SNAKE_OK;
+    }
+    std::lock_guard<std::mutex> g(snake::g_tmu);
+    for (const auto &r : snake::g_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) {
+            snake::set_error("snake_timing_read: event query failed");
+            return SNAKE_E_LAUNCH;
+        }
+        auto &d = snake::g_done[r.name];
+        d.first += ms;
+        d.second += 1;
+        snake::g_pool.push_back(r.a);
+        snake::g_pool.push_back(r.b);
+    }
+    snake::g_pending.clear();
+    auto it = snake::g_done.find(kernel);
+    *total_ms = it == snake::g_done.end() ? 0.0 : it->second.first;
+    *count = it == snake::g_done.end() ? 0 : it->second.second;
+    if (it != snake::g_done.end()) snake::g_done.erase(it);
+    return SNAKE_OK;
+}
 
 #ifdef SNAKE_STAMPS
 extern "C" int snake_debug_obsprof(unsigned long long *out /* 512 */)

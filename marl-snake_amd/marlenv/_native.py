@@ -10,11 +10,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 4
+SNAKE_ABI_VERSION = 5
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
-           'snake_last_error', 'snake_abi_version')
+           'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version')
 
 
 class SnakeCfg(ctypes.Structure):
@@ -80,10 +80,26 @@ def lib(path=None):
                               ctypes.POINTER(SnakeOut), P]
     L.snake_step.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P,
                              ctypes.POINTER(SnakeOut), P]
+    L.snake_timing_enable.argtypes = [ctypes.c_int]
+    L.snake_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                    ctypes.POINTER(ctypes.c_int64)]
     if L.snake_abi_version() != SNAKE_ABI_VERSION:
         raise NativeError('libsnake_amd.so ABI version mismatch; rebuild it')
     _libs[path] = L
     return L
+
+
+def timing_enable(on, L=None):
+    check((L or lib()).snake_timing_enable(1 if on else 0), L)
+
+
+def timing_read(kernel, L=None):
+    """(total device ms, launches) of one kernel since its last read; for
+    kernel='resets' the auto-reset count (ms is 0)."""
+    L = L or lib()
+    ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
+    check(L.snake_timing_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)), L)
+    return ms.value, n.value
 
 
 def check(rc, L=None):

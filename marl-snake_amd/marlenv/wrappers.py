@@ -5,7 +5,9 @@ SingleMultiAgent (or SingleAgent when num_snakes == 1), as wrappers.py:203-223.
 make_snake(num_envs>1, ...) returns a SnakeVecEnv: all envs stepped by one HIP
 launch with all-done auto-reset (the reference forks one gym AsyncVectorEnv
 worker per env, wrappers.py:211-212); its outputs are torch tensors on the GPU.
-RenderGUI / AsyncVectorMultiEnv (OpenCV window, process pool) are out of scope.
+AsyncVectorMultiEnv (the process pool) is replaced by SnakeVecEnv. RenderGUI is
+kept as a pass-through wrapper so callers that import or wrap with it run
+unchanged; drawing an OpenCV window / video is out of scope (render() raises).
 """
 import numpy as np
 
@@ -35,6 +37,16 @@ class Wrapper:
 
     def close(self):
         return self.env.close()
+
+
+class RenderGUI(Wrapper):                         # wrappers.py:20-82
+    def __init__(self, env, window_name='Snake AI', save_video=False, video_path='output.mp4', fps=20):
+        super().__init__(env)
+        self.window_name, self.save_video, self.video_path, self.fps = window_name, save_video, video_path, fps
+
+    def render(self, *args, **kwargs):
+        raise NotImplementedError('RenderGUI windows/videos (OpenCV) are not part of the MI355X build; '
+                                  'env.render() gives an ASCII grid')
 
 
 class SingleAgent(Wrapper):                       # wrappers.py:84-105

@@ -23,7 +23,8 @@ for s in "$@"; do
         testsv) step tests 900 python -m pytest tests -q -m gpu -rf ;;
         bench) step bench 600 python bench.py ;;
         benchq) step bench 300 python bench.py --steps 200 --warmup 50 --cpu-seconds 5 ;;
-        prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 50 --no-cpu-baseline ;;
+        benchnt) step benchnt 300 python bench.py --timing-stride 0 --no-cpu-baseline ;;
+        prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 300 --warmup 100 --no-cpu-baseline ;;
         probe) step probe 600 python scripts/perf_probe.py ;;
         rlat) step rlat 300 python scripts/perf_probe.py --reset-latency ;;
         stamps) step stamps 300 python scripts/reset_stamps.py marl-snake_amd/build/libsnake_stamps.so ;;
@@ -31,10 +32,11 @@ for s in "$@"; do
         ab) step ab 600 python scripts/ab_probe.py marl-snake_amd/build/var/*.so ;;
         ab2) step ab2 600 python scripts/ab_probe.py --cfg cfg2 --N 4096 marl-snake_amd/build/var/*.so ;;
         ab5) step ab5 600 python scripts/ab_probe.py --cfg cfg5 --N 8192 marl-snake_amd/build/var/*.so ;;
-        pmc) step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc1 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
-             step pmc2 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc2 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
-             step pmc3 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc3 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10
-             step pmc4 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE --kernel-include-regex k_step --output-format csv -d gpurun_out/pmc4 -o pmc -- python3 scripts/perf_probe.py --quick --reps 10 ;;
+        pmc) K='k_logic|k_autoreset|k_encode'
+             B='python3 bench.py --steps 40 --warmup 60 --no-cpu-baseline'
+             step pmcF 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcF -o pmc -- $B
+             step pmcW 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcW -o pmc -- $B
+             step pmcSQ 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcSQ -o pmc -- $B ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -43,3 +43,14 @@ def test_shard_ranges():
         for (a, b), (c, d) in zip(spans, spans[1:]):
             assert b == c
         assert sum(b - a for a, b in spans) == N
+
+
+def test_reference_import_paths_resolve():
+    """train_dqn.py:22 / train_ga.py:25 / test_env.py:1 import through the
+    distribution dir: `from marlenv.marlenv.wrappers import make_snake, RenderGUI`."""
+    from marlenv.marlenv.wrappers import RenderGUI, make_snake
+    import marlenv
+    import marlenv.marlenv.envs.snake_env as se
+    assert make_snake is marlenv.make_snake
+    assert se.SnakeEnv is marlenv.SnakeEnv
+    assert issubclass(RenderGUI, marlenv.wrappers.Wrapper)
