@@ -18,6 +18,7 @@
 // reference's order of operations (snake_env.py:365-369, :385-389).
 #include <hip/hip_runtime.h>
 
+#include <limits.h>
 #include <string.h>
 
 #include <map>
@@ -59,6 +60,11 @@ __device__ unsigned long long g_obsprof[512];   // realtime (100 MHz) of auto-re
 #define COUNT_FLUSH(e, lane)                                                       \
     do { if ((e) == 0 && (lane) == 0) { for (int q_ = 0; q_ < 8; q_++) g_counts[q_] += cnt_[q_]; } } while (0)
 #define NOW() __builtin_amdgcn_s_memtime()
+#ifdef SNAKE_STAMPS_ROUNDS
+#define RNOW() __builtin_amdgcn_s_memtime()
+#else
+#define RNOW() 0ull
+#endif
 #else
 #define STAMP(e, lane, idx) do {} while (0)
 #define COUNT(e, lane, idx) do {} while (0)
@@ -66,6 +72,7 @@ __device__ unsigned long long g_obsprof[512];   // realtime (100 MHz) of auto-re
 #define COUNT_ADD(idx, v) do { (void)(v); } while (0)
 #define COUNT_FLUSH(e, lane) do {} while (0)
 #define NOW() 0ull
+#define RNOW() 0ull
 #define OBSPROF(slot, lane) do {} while (0)
 #endif
 
@@ -317,7 +324,7 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
             COUNT(e, lane, 0);
             COUNT_ADD(2, NOW() - t0_);
         }
-        const unsigned long long r0_ = NOW();
+        const unsigned long long r0_ = RNOW();
         COUNT(e, lane, 1);
         const int q = m.pos >> 7, l0 = m.pos & 127;
         const int base = q << 7;
@@ -336,28 +343,27 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
             qc = q;
         }
         const int p0 = lane - l0, p1 = 64 + lane - l0;
-        // valid lanes as uniform masks: ballots of bare compares stay v_cmp -> SGPR
-        const int n1 = min(64, kMtN - base - 64);
-        const unsigned long long vm0 = l0 < 64 ? (~0ull << l0) : 0ull;
-        const unsigned long long vm1 = (n1 == 64 ? ~0ull : ((1ull << n1) - 1ull)) &
-                                       (l0 > 64 ? (~0ull << (l0 - 64)) : ~0ull);
-        const int w0 = (int)(tw0 & mask), w1 = (int)(tw1 & mask);
-        unsigned long long a0 = __ballot(w0 <= i - p0) & vm0, a1 = __ballot(w1 <= i - p1) & vm1;
-        unsigned long long c0 = __ballot(w0 <= i) & vm0, c1 = __ballot(w1 <= i) & vm1;
-        const unsigned long long r2_ = NOW();
+        // words before the stream position or past the key never accept: give them
+        // an impossible value instead of masking every ballot
+        const int w0 = p0 >= 0 ? (int)(tw0 & mask) : INT_MAX;
+        const int w1 = (p1 >= 0 && base + 64 + lane < kMtN) ? (int)(tw1 & mask) : INT_MAX;
+        bool acc0 = w0 <= i - p0, acc1 = w1 <= i - p1;
+        unsigned long long a0 = __ballot(acc0), a1 = __ballot(acc1);
+        unsigned long long c0 = __ballot(w0 <= i), c1 = __ballot(w1 <= i);
+        const unsigned long long r2_ = RNOW();
         COUNT_ADD(4, r2_ - r0_);
         while ((a0 ^ c0) | (a1 ^ c1)) {
             COUNT_ADD(3, 1);
             const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
             const int L1 = __popcll(a0) + mbcnt64(a1), U1 = __popcll(c0) + mbcnt64(c1);
-            const unsigned long long na0 = __ballot(w0 <= i - U0) & vm0;
-            const unsigned long long na1 = __ballot(w1 <= i - U1) & vm1;
-            c0 = __ballot(w0 <= i - L0) & vm0;
-            c1 = __ballot(w1 <= i - L1) & vm1;
-            a0 = na0;
-            a1 = na1;
+            acc0 = w0 <= i - U0;
+            acc1 = w1 <= i - U1;
+            c0 = __ballot(w0 <= i - L0);
+            c1 = __ballot(w1 <= i - L1);
+            a0 = __ballot(acc0);
+            a1 = __ballot(acc1);
         }
-        const unsigned long long r3_ = NOW();
+        const unsigned long long r3_ = RNOW();
         COUNT_ADD(5, r3_ - r2_);
         int A0 = __popcll(a0);
         int A = A0 + __popcll(a1);
@@ -365,28 +371,30 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
         const int k = i - lo + 1;  // accepts left in this bracket
         if (A >= k) {
             if (A0 >= k) {
-                const int b = __ffsll((long long)__ballot(((a0 >> lane) & 1ull) && mbcnt64(a0) == k - 1)) - 1;
+                const int b = __ffsll((long long)__ballot(acc0 && mbcnt64(a0) == k - 1)) - 1;
+                acc0 = acc0 && lane <= b;
+                acc1 = false;
                 a0 &= (2ull << b) - 1ull;
                 a1 = 0;
                 A0 = k;
                 end = b + 1;
             } else {
                 const int k1 = k - A0;
-                const int b = __ffsll((long long)__ballot(((a1 >> lane) & 1ull) && mbcnt64(a1) == k1 - 1)) - 1;
+                const int b = __ffsll((long long)__ballot(acc1 && mbcnt64(a1) == k1 - 1)) - 1;
+                acc1 = acc1 && lane <= b;
                 a1 &= (2ull << b) - 1ull;
                 end = 64 + b + 1;
             }
             A = k;
         }
         const int ii0 = i - mbcnt64(a0), ii1 = i - A0 - mbcnt64(a1);
-        const bool r0 = (a0 >> lane) & 1ull, r1 = (a1 >> lane) & 1ull;
         if (i - A + 1 >= S) {
             // every index of the round >= S: unconditional ds_min, misses to the dummy
-            link_min((r0 && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
-            link_min((r1 && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
+            link_min((acc0 && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
+            link_min((acc1 && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
         } else {
-            if (r0) perm_record(ii0, w0, S, link, jsmall);
-            if (r1) perm_record(ii1, w1, S, link, jsmall);
+            if (acc0) perm_record(ii0, w0, S, link, jsmall);
+            if (acc1) perm_record(ii1, w1, S, link, jsmall);
         }
         m.pos = base + end;
         i -= A;
@@ -394,7 +402,7 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
             mask = gen_mask((uint32_t)i);
             lo = (int)(mask >> 1) + 1;
         }
-        COUNT_ADD(6, NOW() - r3_);
+        COUNT_ADD(6, RNOW() - r3_);
     }
     COUNT_FLUSH(e, lane);
 }
@@ -654,35 +662,56 @@ __device__ __forceinline__ void stage_to_lds(uint8_t *dst, const uint8_t *src, i
 }
 
 // ---------------------------------------------------------- step: the rules
-// k_logic: one wave per env runs SnakeEnv.step up to the observation: rules,
-// grid update, fruit respawn, statistics and outputs; the new frame goes to its
-// ring slot; an env whose episode ended is queued for its auto-reset.
+// k_logic runs SnakeEnv.step up to the observation -- rules, grid update, fruit
+// respawn, statistics and outputs -- for E = 64 / MS envs per wave: lane
+// (g, k) = snake k of the block's env g, so the per-snake rules of 16 (S <= 4),
+// 8 or 4 envs share every instruction and every memory round trip. The new
+// frame goes to its ring slot; an env whose episode ended is queued for its
+// auto-reset. The wave-wide parts (dying-body erase, fruit respawn) loop over the
+// block's envs that need them.
 template <int MS>
 __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c, const snake_state st,
                                                               const int8_t *__restrict__ actions,
                                                               const snake_out o, int parity)
 {
+    constexpr int G = MS, E = kWave / MS;
+    constexpr uint32_t gmask = (1u << G) - 1u;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int e = blockIdx.x, lane = threadIdx.x;
+    const int lane = threadIdx.x, g = lane / G, k = lane - g * G, gb = g * G;
+    const int e0 = blockIdx.x * E, e = e0 + g;
     const int S = c.S, W = c.W, cap = c.ring_cap, fs = c.fs, stride = c.grid_stride;
-    uint8_t *work = lds;                                   // the grid being stepped
-    uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + stride);
-    const bool isn = lane < S;
-    if (e == 0 && lane == 0) st.resetq[c.N + (parity ^ 1)] = 0;   // next step's queue
+    const int n16 = stride >> 4;
+    const bool env_ok = e < c.N;
+    const bool isn = env_ok && k < S;
+    uint8_t *work = lds + g * stride;                      // this env's grid being stepped
+    uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + E * stride);
+    if (blockIdx.x == 0 && lane == 0) st.resetq[c.N + (parity ^ 1)] = 0;   // next step's queue
+    auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
-    // ---- every load this step needs, issued up front (one memory round trip)
-    const int4 er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
+    // ---- every load this step needs, issued up front
+    int4 er = make_int4(0, 0, 0, 0);
+    if (env_ok) er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
     int4 rec = make_int4(0, 0, 0, 0);
     int act = 0;
     double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     double *sp = st.stats + (int64_t)e * 4 * S;
     if (isn) {
-        rec = reinterpret_cast<const int4 *>(st.snake)[(int64_t)e * S + lane];
-        act = actions[(int64_t)e * S + lane];
-        s0 = sp[lane]; s1 = sp[S + lane]; s2 = sp[2 * S + lane]; s3 = sp[3 * S + lane];
+        rec = reinterpret_cast<const int4 *>(st.snake)[(int64_t)e * S + k];
+        act = actions[(int64_t)e * S + k];
+        s0 = sp[k]; s1 = sp[S + k]; s2 = sp[2 * S + k]; s3 = sp[3 * S + k];
     }
     const int alive0 = er.x, eplen = er.y, cur = er.z, mtpos = er.w;
-    stage_to_lds(work, st.grid + (int64_t)e * c.ring_bytes + cur * stride, stride, lane);
+    {   // stage the E current frames: env g's at lds + g * stride
+        const uint4 *src = reinterpret_cast<const uint4 *>(st.grid);
+        uint4 *d4 = reinterpret_cast<uint4 *>(lds);
+        // uniform trip count: __shfl must not read from lanes a divergent loop parked
+        for (int q0 = 0; q0 < E * n16; q0 += kWave) {
+            const int q = q0 + lane, gg = min(q / n16, E - 1), off = q - gg * n16;
+            const int cg = __shfl(cur, gg * G);
+            if (q < E * n16 && e0 + gg < c.N)
+                d4[q] = src[((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)cg * stride) / 16 + off];
+        }
+    }
     const int ncur = (fs == 1) ? 0 : (cur + 1 == fs ? 0 : cur + 1);
     int hr = rec.x & 255, hc = (rec.x >> 8) & 255, tr = (rec.x >> 16) & 255, tc = (rec.x >> 24) & 255;
     int dir = rec.y & 3, alive = (rec.y >> 8) & 1;
@@ -690,7 +719,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const int tdir = rec.w;                   // cached directions[-1] (core/snake.py:103)
 
     // snake_env.py:318-330 heading + target cell per alive snake
-    const bool mv = isn && alive;
+    const bool mv0 = isn && alive;
     int nd = dir;
     if (c.observer == 0) {                 // _next_direction :598-608 (0 keep, 1 left, 2 right)
         nd = (act == 1) ? ((dir + 3) & 3) : ((act == 2) ? ((dir + 1) & 3) : dir);
@@ -699,10 +728,11 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     } else {
         nd = (act == 1) ? 3 : ((act == 2) ? 1 : dir);
     }
-    if (__ballot(mv && c.observer == 0 && (act < 0 || act > 2))) {
-        if (lane == 0) { o.err[e] = 1; o.ep_done[e] = 0; }   // KeyError: env untouched
-        return;
-    }
+    // an invalid action of an alive snake raises KeyError in the reference before
+    // anything changes: that env is left untouched (only err/ep_done are written)
+    const bool bad = gbits(__ballot(mv0 && c.observer == 0 && (act < 0 || act > 2))) != 0u;
+    const bool live = isn && !bad;
+    const bool mv = mv0 && !bad;
     if (mv) dir = nd;
     const int ncell = mv ? (hr + dir_dr(dir)) * W + hc + dir_dc(dir) : -1 - lane;
     wave_sync();
@@ -711,9 +741,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     int cnt = 0;
     bool lower = false;
     for (int j = 0; j < S; j++) {
-        const bool same = bcast(ncell, j) == ncell;
+        const bool same = __shfl(ncell, gb + j) == ncell;
         cnt += same;
-        lower |= same && j < lane;
+        lower |= same && j < k;
     }
     const bool leader = mv && !lower;
     const int v = mv ? work[ncell] : 0;
@@ -722,25 +752,26 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const bool eat = mv && !deadly && cv == C_FRUIT;
     // every target group on a fruit cell counts once: an eater, or a head-on there
     // (the fruit stays and one more spawns)
-    const int fruit_taken = __popcll(__ballot(leader && cv == C_FRUIT));
+    const int fruit_taken = __popc(gbits(__ballot(leader && cv == C_FRUIT)));
     // kill credit: one per deadly group on a BODY/HEAD cell, to its owner (self too)
     const int owner = (leader && deadly && (cv == C_BODY || cv == C_HEAD)) ? vid : -1;
     int kills = 0;
-    for (int j = 0; j < S; j++) kills += bcast(owner, j) == lane;
-    int alive_snakes = alive0 - __popcll(__ballot(deadly));                  // :334
+    for (int j = 0; j < S; j++) kills += __shfl(owner, gb + j) == k;
+    int alive_snakes = alive0 - __popc(gbits(__ballot(deadly)));            // :334
     bool death = deadly;
     // :338-346 a fruit eater's tail does not move: snakes entering it die (again)
     const int etail = eat ? tr * W + tc : -2;
     bool hit = false;
     for (int j = 0; j < S; j++) {
-        hit |= mv && bcast(etail, j) == ncell;
-        kills += (eat && bcast(ncell, j) == etail) ? 1 : 0;
+        const int ej = __shfl(etail, gb + j), nj = __shfl(ncell, gb + j);
+        hit |= mv && ej == ncell;
+        kills += (eat && nj == etail) ? 1 : 0;
     }
-    alive_snakes -= __popcll(__ballot(hit));
+    alive_snakes -= __popc(gbits(__ballot(hit)));
     death |= hit;
     alive = mv && !death;
-    const unsigned long long am = __ballot(isn && alive);
-    const bool win = alive_snakes == 1 && S > 1 && am && lane == __ffsll((long long)am) - 1;
+    const uint32_t am = gbits(__ballot(isn && alive));
+    const bool win = alive_snakes == 1 && S > 1 && am && k == __ffs(am) - 1;
 
     // rewards, fp64 in the reference order (:354-370)
     const bool counted = death || alive;   // not previously dead
@@ -762,16 +793,16 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // which is what the reference's index-ordered updates produce.
     const int pt = tr * W + tc;
     if (alive && !eat) {
-        if (work[pt] == C_TAIL + 10 * lane) work[pt] = C_EMPTY;
+        if (work[pt] == C_TAIL + 10 * k) work[pt] = C_EMPTY;
     }
     if (isn && death) {
-        if (div10(work[pt]) == lane) work[pt] = C_EMPTY;
+        if (div10(work[pt]) == k) work[pt] = C_EMPTY;
     }
     wave_sync();
-    uint8_t *ring = st.body + ((int64_t)e * S + lane) * cap;
+    uint8_t *ring = st.body + ((int64_t)e * S + k) * cap;
     int nhr = hr, nhc = hc, ntr = tr, ntc = tc, ntdir = tdir;
     if (alive) {
-        work[hr * W + hc] = (uint8_t)(C_BODY + 10 * lane);
+        work[hr * W + hc] = (uint8_t)(C_BODY + 10 * k);
         nhr = hr + dir_dr(dir);
         nhc = hc + dir_dc(dir);
         rh = (rh - 1) & (cap - 1);                                   // directions.appendleft
@@ -784,40 +815,49 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         } else {
             rl++;
         }
-        work[nhr * W + nhc] = (uint8_t)(C_HEAD + 10 * lane);
-        work[ntr * W + ntc] = (uint8_t)(C_TAIL + 10 * lane);
+        work[nhr * W + nhc] = (uint8_t)(C_HEAD + 10 * k);
+        work[ntr * W + ntc] = (uint8_t)(C_TAIL + 10 * k);
     }
     wave_sync();
     // draw(grid, coords, EMPTY) of each dying snake's head and body (the tail was
     // handled above): coords = head - prefix sums of the direction deque
-    // (core/snake.py:86-94), 64 cells per pass.
+    // (core/snake.py:86-94), 64 cells per pass, one dying snake at a time.
     unsigned long long dm = __ballot(isn && death);
     while (dm) {
-        const int k = __ffsll((long long)dm) - 1;
+        const int L = __ffsll((long long)dm) - 1;
         dm &= dm - 1;
-        const int khr = bcast(hr, k), khc = bcast(hc, k), krh = bcast(rh, k), krl = bcast(rl, k);
-        const uint8_t *kring = st.body + ((int64_t)e * S + k) * cap;
+        const int gg = L / G, kk = L - gg * G;
+        const int khr = bcast(hr, L), khc = bcast(hc, L), krh = bcast(rh, L), krl = bcast(rl, L);
+        const uint8_t *kring = st.body + ((int64_t)(e0 + gg) * S + kk) * cap;
+        uint8_t *gw = lds + gg * stride;
         int br = khr, bc = khc;
-        if (lane == 0) work[khr * W + khc] = C_EMPTY;
+        if (lane == 0) gw[khr * W + khc] = C_EMPTY;
         for (int m0 = 0; m0 < krl - 1; m0 += kWave) {
             const int m = m0 + lane;
             const bool ok = m < krl - 1;
             const int d = ok ? kring[(krh + m) & (cap - 1)] : 0;
             const int sr = wave_scan(ok ? dir_dr(d) : 0, lane);
             const int sc = wave_scan(ok ? dir_dc(d) : 0, lane);
-            if (ok) work[(br - sr) * W + (bc - sc)] = C_EMPTY;
+            if (ok) gw[(br - sr) * W + (bc - sc)] = C_EMPTY;
             br -= bcast(sr, 63);
             bc -= bcast(sc, 63);
         }
     }
     wave_sync();
 
-    WaveMT mt;
-    bool mt_loaded = false;
-    if (fruit_taken > 0) {                                         // :376-379
-        mt_load(mt, st.mt + (int64_t)e * kMtN, mtpos, lane);
-        mt_loaded = true;
-        place_fruits(c, work, mt, fruit_taken, fbuf, lane);
+    // fruit respawn (:376-379), one env at a time with the whole wave
+    int mtpos_new = mtpos;
+    unsigned long long fm = __ballot(live && k == 0 && fruit_taken > 0);
+    while (fm) {
+        const int L = __ffsll((long long)fm) - 1;
+        fm &= fm - 1;
+        const int gg = L / G;
+        const int64_t ee = e0 + gg;
+        WaveMT mt;
+        mt_load(mt, st.mt + ee * kMtN, bcast(mtpos, L), lane);
+        place_fruits(c, lds + gg * stride, mt, bcast(fruit_taken, L), fbuf, lane);
+        mt_store(mt, st.mt + ee * kMtN, lane);
+        if (g == gg) mtpos_new = mt.pos;
     }
 
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
@@ -831,54 +871,61 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     }
     const int eplen1 = eplen + 1;
     int fd = ((double)eplen1 >= c.max_steps) ? 1 : dn;
-    const unsigned long long done_m = __ballot(isn && fd);
-    const unsigned long long all_m = (S >= 64) ? ~0ull : ((1ull << S) - 1ull);
-    const bool ep_end = c.coop ? (done_m != 0ull) : (done_m == all_m);
+    const uint32_t done_m = gbits(__ballot(isn && fd));
+    const uint32_t all_m = (1u << S) - 1u;
+    const bool ep_end = !bad && (c.coop ? (done_m != 0u) : (done_m == all_m));
     if (c.coop && ep_end) fd = 1;
-    if (isn) {
-        o.rew[(int64_t)e * S + lane] = rew;
-        o.done[(int64_t)e * S + lane] = (uint8_t)fd;
+    if (live) {
+        o.rew[(int64_t)e * S + k] = rew;
+        o.done[(int64_t)e * S + k] = (uint8_t)fd;
     }
-    if (lane == 0) {
+    if (env_ok && k == 0) {
         o.ep_done[e] = ep_end ? 1 : 0;
-        o.err[e] = 0;
+        o.err[e] = bad ? 1 : 0;
         if (ep_end && c.autoreset) {                  // queue the auto-reset
             const int slot = atomicAdd(&st.resetq[c.N + parity], 1);
             st.resetq[slot] = e;
         }
     }
+    int rank = 1;
+    for (int j = 0; j < S; j++) rank += (__shfl(s0, gb + j) > s0);
     if (ep_end) {
-        int rank = 1;
-        for (int j = 0; j < S; j++) rank += (__shfl(s0, j) > s0);
         if (isn) {
-            o.rank[(int64_t)e * S + lane] = rank;
+            o.rank[(int64_t)e * S + k] = rank;
             double *es = o.ep_stats + (int64_t)e * 4 * S;
-            es[lane] = s0; es[S + lane] = s1; es[2 * S + lane] = s2; es[3 * S + lane] = s3;
+            es[k] = s0; es[S + k] = s1; es[2 * S + k] = s2; es[3 * S + k] = s3;
         }
         s0 = s1 = s2 = s3 = 0.0;                                   // _reset_epi_stats
     }
-    if (isn) { sp[lane] = s0; sp[S + lane] = s1; sp[2 * S + lane] = s2; sp[3 * S + lane] = s3; }
+    if (live) { sp[k] = s0; sp[S + k] = s1; sp[2 * S + k] = s2; sp[3 * S + k] = s3; }
 
-    // commit the new frame into its ring slot; records; crop centre of the frame
-    uint8_t *gdst = st.grid + (int64_t)e * c.ring_bytes + ncur * stride;
-    for (int q = lane; q < (stride >> 4); q += kWave)
-        reinterpret_cast<uint4 *>(gdst)[q] = reinterpret_cast<const uint4 *>(work)[q];
+    // commit the new frames into their ring slots; records; crop centres
+    {
+        uint4 *dst = reinterpret_cast<uint4 *>(st.grid);
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(lds);
+        for (int q0 = 0; q0 < E * n16; q0 += kWave) {
+            const int q = q0 + lane, gg = min(q / n16, E - 1), off = q - gg * n16;
+            const int ng = __shfl(ncur, gg * G);
+            const int bg = __shfl((int)bad, gg * G);
+            if (q < E * n16 && e0 + gg < c.N && !bg)
+                dst[((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)ng * stride) / 16 + off] = s4[q];
+        }
+    }
     // crop centre = the own HEAD cell: the new head while alive, (0,0) when dead
     const int chr = alive ? nhr : 0, chc = alive ? nhc : 0;
-    if (lane == 0) {
+    if (env_ok && k == 0 && !bad) {
         int4 ner;
-        ner.x = alive_snakes; ner.y = eplen1; ner.z = ncur; ner.w = mt_loaded ? mt.pos : mtpos;
+        ner.x = alive_snakes; ner.y = eplen1; ner.z = ncur; ner.w = mtpos_new;
         *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = ner;
     }
-    if (mt_loaded) mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
-    if (isn) {
-        st.ctr[((int64_t)e * fs + ncur) * S + lane] = (uint16_t)((chr << 8) | chc);
+    if (live) {
+        st.ctr[((int64_t)e * fs + ncur) * S + k] = (uint16_t)((chr << 8) | chc);
         int4 nrec;
         nrec.x = nhr | (nhc << 8) | (ntr << 16) | (ntc << 24);
         nrec.y = dir | (alive << 8);
         nrec.z = rh | (rl << 16);
         nrec.w = ntdir;
-        reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + lane] = nrec;
+        reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + k] = nrec;
     }
 }
 
@@ -1086,12 +1133,13 @@ int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, con
                 int parity, void *stream)
 {
     const hipStream_t sm = (hipStream_t)stream;
-    const int lds_logic = k.grid_stride + 2 * kMaxFruits;
-    const dim3 g1(k.N), gr(k.reset_slots), block(kWave);
+    const int ms = k.S <= 4 ? 4 : (k.S <= 8 ? 8 : 16), epw = kWave / ms;   // envs per k_logic wave
+    const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits;
+    const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
     TimedLaunch t1("k_logic", sm);
-    if (k.S <= 4) hipLaunchKernelGGL(k_logic<4>, g1, block, lds_logic, sm, k, st, actions, o, parity);
-    else if (k.S <= 8) hipLaunchKernelGGL(k_logic<8>, g1, block, lds_logic, sm, k, st, actions, o, parity);
-    else hipLaunchKernelGGL(k_logic<16>, g1, block, lds_logic, sm, k, st, actions, o, parity);
+    if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, k, st, actions, o, parity);
+    else if (ms == 8) hipLaunchKernelGGL(k_logic<8>, gl, block, lds_logic, sm, k, st, actions, o, parity);
+    else hipLaunchKernelGGL(k_logic<16>, gl, block, lds_logic, sm, k, st, actions, o, parity);
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;

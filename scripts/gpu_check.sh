@@ -28,6 +28,7 @@ for s in "$@"; do
         probe) step probe 600 python scripts/perf_probe.py ;;
         rlat) step rlat 300 python scripts/perf_probe.py --reset-latency ;;
         stamps) step stamps 300 python scripts/reset_stamps.py marl-snake_amd/build/libsnake_stamps.so ;;
+        lat) step lat 120 scripts/microbench/lat ;;
         obsprof) step obsprof 300 python scripts/obs_profile.py marl-snake_amd/build/libsnake_stamps.so ;;
         ab) step ab 600 python scripts/ab_probe.py marl-snake_amd/build/var/*.so ;;
         ab2) step ab2 600 python scripts/ab_probe.py --cfg cfg2 --N 4096 marl-snake_amd/build/var/*.so ;;
