@@ -63,7 +63,7 @@ typedef struct {
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
     int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
     int64_t jscratch;   /* uint32 [min(N,2048)][round4(n_cand)+64] reset link tables, 0 if in LDS */
-    int64_t resetq;     /* int32  [N + 2]                auto-reset queue + two counters */
+    int64_t resetq;     /* int32  [64][cap] + [2][64]    sharded auto-reset queue + counters */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */
     int64_t rew;        /* double [N][S] */
     int64_t done;       /* uint8  [N][S] */

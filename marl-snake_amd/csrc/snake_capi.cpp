@@ -201,7 +201,13 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     // when small, else one global table per reset worker.
     const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
     o->jscratch = (link <= kLinkLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
-    o->resetq = (N + 2) * 4;
+    {   // auto-reset queue: kQShards shards (k_logic block % kQShards), each with room
+        // for every env of its blocks, + two parities of per-shard counters
+        const int64_t E = kWave / (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
+        const int64_t blocks = (N + E - 1) / E;
+        const int64_t cap = (blocks + kQShards - 1) / kQShards * E;
+        o->resetq = (kQShards * cap + 2 * kQShards) * 4;
+    }
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
     o->done = N * S;
@@ -252,11 +258,31 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->lds_frames = off; off += (int)round_up((int64_t)k->fs * k->grid_stride, 16);
     k->lds_centers = off; off += (int)round_up(4 * k->fs * kMaxSnakes, 16);
     k->lds_fruit = off; off += (int)round_up(2 * kMaxFruits, 16);
+    {   // staged encode: whole snakes per group, every group start 16-byte aligned
+        const int64_t P = (int64_t)k->oh * k->ow * 8 * k->fs;       // obs bytes per snake
+        int g = 0;
+        if ((int64_t)k->S * P <= kStageMax) {
+            g = k->S;
+        } else {
+            g = (int)std::min<int64_t>(k->S, kStageMax / P);
+            if (P % 16 != 0) g &= ~1;
+        }
+        k->enc_group = g;
+        k->lds_stage = off;
+        if (g > 0) off += (int)round_up(g * P, 16);
+        const uint64_t fsoh = (uint64_t)k->fs * k->oh, oh = (uint64_t)k->oh;
+        k->mag_fsoh = (uint32_t)(((1ull << 32) + fsoh - 1) / fsoh);
+        k->mag_oh = (uint32_t)(((1ull << 32) + oh - 1) / oh);
+    }
     k->link_stride = (int)round_up(k->n_cand, 4) + kWave;
     k->link_in_lds = 4 * k->link_stride <= kLinkLdsMax;
     k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
+    k->q_envs_per_block = kWave / (k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16));
+    {
+        const int64_t blocks = (N + k->q_envs_per_block - 1) / k->q_envs_per_block;
+        k->q_cap = (int)((blocks + kQShards - 1) / kQShards * k->q_envs_per_block);
+    }
     k->lds_obs_bytes = off;
-    k->lds_mtt = off; off += 4 * 640;
     k->lds_link = off;
     if (k->link_in_lds) off += 4 * k->link_stride;
     k->lds_bytes = off;

@@ -14,6 +14,8 @@ constexpr int kMaxFruits = 64;
 constexpr int kEnvRec = 8;          // int32 words per env record
 constexpr int kLinkLdsMax = 16384;  // bytes of a reset link table kept in LDS
 constexpr int kResetSlots = 2048;   // concurrent reset workers (global link tables)
+constexpr int kQShards = 64;        // auto-reset queue shards (k_logic block % 64)
+constexpr int kStageMax = 8192;     // bytes of staged observation per encode group
 
 // env record words
 enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3 };
@@ -31,9 +33,15 @@ struct KCfg {
     // dynamic LDS carve (bytes, 16-aligned)
     int lds_frames, lds_centers, lds_fruit, lds_link, lds_bytes, link_in_lds;
     int link_stride;            // round4(n_cand) + 64 per-lane dummies: u32 entries of a link table
-    int lds_mtt;                // tempered MT block (640 u32) of a reset worker
     int lds_obs_bytes;          // LDS of k_encode: no reset worker state
+    // row-wise encode through an LDS staging buffer (encode_rows): snakes per
+    // staged group (0: direct encode), the buffer, and magic reciprocals of
+    // fs*oh and oh (x / d == umulhi(x, m) for the row indices used)
+    int enc_group, lds_stage;
+    uint32_t mag_fsoh, mag_oh;
     int reset_slots;            // min(N, kResetSlots)
+    int q_envs_per_block;       // envs per k_logic block (64 / MS)
+    int q_cap;                  // queue entries per shard
     double rf, rk, rl, rw, rt, max_steps;
 };
 

@@ -60,6 +60,15 @@ __device__ unsigned long long g_obsprof[512];   // realtime (100 MHz) of auto-re
 #define COUNT_FLUSH(e, lane)                                                       \
     do { if ((e) == 0 && (lane) == 0) { for (int q_ = 0; q_ < 8; q_++) g_counts[q_] += cnt_[q_]; } } while (0)
 #define NOW() __builtin_amdgcn_s_memtime()
+#define LSTAMP(idx)                                                                \
+    do {                                                                           \
+        if (blockIdx.x == 0) {                                                     \
+            __builtin_amdgcn_sched_barrier(0);                                     \
+            unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
+            if (threadIdx.x == 0) g_stamps[idx] = _t;                              \
+            __builtin_amdgcn_sched_barrier(0);                                     \
+        }                                                                          \
+    } while (0)
 #ifdef SNAKE_STAMPS_ROUNDS
 #define RNOW() __builtin_amdgcn_s_memtime()
 #else
@@ -72,6 +81,7 @@ __device__ unsigned long long g_obsprof[512];   // realtime (100 MHz) of auto-re
 #define COUNT_ADD(idx, v) do { (void)(v); } while (0)
 #define COUNT_FLUSH(e, lane) do {} while (0)
 #define NOW() 0ull
+#define LSTAMP(idx) do {} while (0)
 #define RNOW() 0ull
 #define OBSPROF(slot, lane) do {} while (0)
 #endif
@@ -290,18 +300,9 @@ __device__ __forceinline__ void perm_record(int ii, int w, int S, NP *link, lu16
     else if (w != ii) link_min(link + w, (uint32_t)ii);
 }
 
-// The tempered key block, 640 words (the last 16 are never valid), in LDS: a
-// round reads its register pair with two ds_read_b32 instead of selecting it out
-// of the key registers.
-__device__ __forceinline__ void temper_block(const WaveMT &m, lu32 *mtt, int lane)
-{
-#pragma unroll
-    for (int t = 0; t < 10; t++) mtt[64 * t + lane] = temper(m.w[t]);
-}
-
 template <typename NP>
-__device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, lu32 *mtt,
-                              int lane, int e = -1)
+__device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, int lane,
+                              int e = -1)
 {
     int i = n - 1;
     if (i < 1) return;
@@ -310,17 +311,20 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
     int lo = (int)(mask >> 1) + 1;
     // lanes with nothing to record write their own dummy entry past the table
     NP *dummy = link + link_n + lane;
-    // the current register pair and the next one, read ahead so that the LDS
-    // atomics of a round are never waited for by the next round's reads
-    int qc = -2;   // -2: nothing read ahead
-    uint32_t tw0 = 0, tw1 = 0, nx0 = 0, nx1 = 0;
-    if (m.pos < kMtN) temper_block(m, mtt, lane);
+    // the tempered key stays in registers: the rounds never read LDS, so nothing
+    // waits for the link-table atomics until the draws are done
+    uint32_t tk[10];
+#pragma unroll
+    for (int t = 0; t < 10; t++) tk[t] = temper(m.w[t]);
+    int qc = -1;
+    uint32_t tw0 = 0, tw1 = 0;
     while (i >= 1) {
         if (m.pos >= kMtN) {
             const unsigned long long t0_ = NOW();
             mt_twist(m, lane);
-            temper_block(m, mtt, lane);
-            qc = -2;
+#pragma unroll
+            for (int t = 0; t < 10; t++) tk[t] = temper(m.w[t]);
+            qc = -1;
             COUNT(e, lane, 0);
             COUNT_ADD(2, NOW() - t0_);
         }
@@ -329,17 +333,15 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
         const int q = m.pos >> 7, l0 = m.pos & 127;
         const int base = q << 7;
         if (q != qc) {
-            if (q == qc + 1) {
-                tw0 = nx0;
-                tw1 = nx1;
-            } else {
-                tw0 = mtt[base + lane];
-                tw1 = mtt[base + 64 + lane];
+            uint32_t a = 0, b = 0;
+#pragma unroll
+            for (int r = 0; r < 5; r++) {
+                const uint32_t sel = 0u - (uint32_t)(q == r);
+                a |= tk[2 * r] & sel;
+                b |= tk[2 * r + 1] & sel;
             }
-            if (q < 4) {
-                nx0 = mtt[base + 128 + lane];
-                nx1 = mtt[base + 192 + lane];
-            }
+            tw0 = a;
+            tw1 = b;
             qc = q;
         }
         const int p0 = lane - l0, p1 = 64 + lane - l0;
@@ -532,6 +534,61 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
     }
 }
 
+// Row-wise encode: lane = one (snake, frame, window row); the row's cells are
+// scattered as single bytes into a zeroed LDS image of a group of whole snakes'
+// observations, which is then copied out with 16-byte stores. Per cell: one
+// frame byte read, the channel, one byte write (empty cells write nothing).
+__device__ void encode_rows(const KCfg &c, const uint8_t *frames, const int *org, int slot0,
+                            uint8_t *obs_env, uint8_t *stage, int lane)
+{
+    const int fs = c.fs, ow = c.ow, oh = c.oh, S = c.S, cellb = 8 * fs, W = c.W;
+    const int P = oh * ow * cellb;
+    const int fsoh = fs * oh;
+    const bool wide = (c.units & 1) == 0;
+    for (int k0 = 0; k0 < S; k0 += c.enc_group) {
+        const int gs = min(c.enc_group, S - k0), bytes = gs * P;
+        for (int q = lane; q < (bytes + 15) >> 4; q += kWave)
+            reinterpret_cast<uint4 *>(stage)[q] = make_uint4(0, 0, 0, 0);
+        wave_sync();
+        for (int rr = lane; rr < gs * fsoh; rr += kWave) {
+            const int kk = (int)__umulhi((uint32_t)rr, c.mag_fsoh), rem = rr - kk * fsoh;
+            const int f = (int)__umulhi((uint32_t)rem, c.mag_oh), i = rem - f * oh;
+            const int k = k0 + kk;
+            int s = slot0 + f;
+            s -= (s >= fs) ? fs : 0;
+            const int p = org[s * kMaxSnakes + k];
+            const int r = (p >> 16) - 256 + i, c0 = (p & 0xffff) - 256;
+            if ((unsigned)r >= (unsigned)c.H) continue;
+            const uint8_t *row = frames + s * c.grid_stride + r * W;
+            uint8_t *dst = stage + kk * P + i * ow * cellb + f * 8;
+            for (int j = 0; j < ow; j++) {
+                const int cc = c0 + j;
+                const int v = ((unsigned)cc < (unsigned)W) ? row[cc] : 0;
+                const int id = div10(v), code = v - 10 * id;
+                const int ch = (v < 3) ? v - 1 : code - 1 + ((id == k) ? 3 : 0);
+                if (v != 0) dst[j * cellb + ch] = 1;
+            }
+        }
+        wave_sync();
+        uint8_t *out = obs_env + (int64_t)k0 * P;
+        if (wide) {
+            for (int q = lane; q < bytes >> 4; q += kWave)
+                reinterpret_cast<uint4 *>(out)[q] = reinterpret_cast<const uint4 *>(stage)[q];
+        } else {
+            for (int q = lane; q < bytes >> 3; q += kWave)
+                reinterpret_cast<uint2 *>(out)[q] = reinterpret_cast<const uint2 *>(stage)[q];
+        }
+        wave_sync();
+    }
+}
+
+__device__ __forceinline__ void encode_obs(const KCfg &c, const uint8_t *frames, const int *org, int slot0,
+                                           uint8_t *obs_env, uint8_t *lds, int lane)
+{
+    if (c.enc_group > 0) encode_rows(c, frames, org, slot0, obs_env, lds + c.lds_stage, lane);
+    else encode(c, frames, org, slot0, obs_env, lane);
+}
+
 __device__ __forceinline__ int pack_origin(const KCfg &c, int r, int cc)
 {
     return c.vr ? (((r - c.vr + 256) << 16) | (cc - c.vr + 256)) : ((256 << 16) | 256);
@@ -569,7 +626,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         for (int x = 4 * lane; x < c.link_stride - kWave; x += 4 * kWave)
             *(typename std::conditional<JL, lu4, gu4>::type *)(link + x) = (v4u32)kNoLink;
         if (JL) wave_sync(); else __syncthreads();
-        mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, (lu32 *)(lds + c.lds_mtt), lane, e);
+        mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, lane, e);
         STAMP(e, lane, 2 + 3 * min(attempt, 3));
         if (JL) wave_sync(); else __syncthreads();   // the link table, written by every lane
         int q[MS];
@@ -636,6 +693,8 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
     wave_sync();
     STAMP(e, lane, 22);
+    // (the direct encode: one env's obs is on the reset's critical path, where the
+    // staged row-wise encode's two extra LDS passes cost more than they save)
     encode(c, frames, org, 0, o.obs + (int64_t)e * c.units * 8, lane);
     STAMP(e, lane, 23);
 }
@@ -685,7 +744,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const bool isn = env_ok && k < S;
     uint8_t *work = lds + g * stride;                      // this env's grid being stepped
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + E * stride);
-    if (blockIdx.x == 0 && lane == 0) st.resetq[c.N + (parity ^ 1)] = 0;   // next step's queue
+    int *qcnt = st.resetq + kQShards * c.q_cap;                       // [2][kQShards]
+    if (blockIdx.x == 0) qcnt[(parity ^ 1) * kQShards + lane] = 0;   // next step's counters
+    LSTAMP(40);
     auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
     // ---- every load this step needs, issued up front
@@ -736,6 +797,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     if (mv) dir = nd;
     const int ncell = mv ? (hr + dir_dr(dir)) * W + hc + dir_dc(dir) : -1 - lane;
     wave_sync();
+    LSTAMP(41);
 
     // _check_collision :521-544 -- groups of snakes with the same target cell
     int cnt = 0;
@@ -773,6 +835,21 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const uint32_t am = gbits(__ballot(isn && alive));
     const bool win = alive_snakes == 1 && S > 1 && am && k == __ffs(am) - 1;
 
+    // episode end (:391-394 truncation, coop any-done) is known here: claim the
+    // auto-reset queue slots now, one atomic per wave on this block's shard, so the
+    // atomic's round trip overlaps the rest of the step
+    const int eplen1 = eplen + 1;
+    const int dn = !alive;
+    int fd = ((double)eplen1 >= c.max_steps) ? 1 : dn;
+    const uint32_t done_m = gbits(__ballot(isn && fd));
+    const uint32_t all_m = (1u << S) - 1u;
+    const bool ep_end = !bad && (c.coop ? (done_m != 0u) : (done_m == all_m));
+    if (c.coop && ep_end) fd = 1;
+    const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && ep_end) : 0ull;
+    const int shard = blockIdx.x % kQShards;
+    int qbase = 0;
+    if (qm && lane == 0) qbase = atomicAdd(&qcnt[parity * kQShards + shard], __popcll(qm));
+
     // rewards, fp64 in the reference order (:354-370)
     const bool counted = death || alive;   // not previously dead
     double rew = 0.0;
@@ -791,6 +868,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // new head, TAIL at the new tail. Phase-2 cells are pairwise distinct and a
     // phase-1 cell is rewritten in phase 2 only by a snake entering that tail,
     // which is what the reference's index-ordered updates produce.
+    LSTAMP(42);
     const int pt = tr * W + tc;
     if (alive && !eat) {
         if (work[pt] == C_TAIL + 10 * k) work[pt] = C_EMPTY;
@@ -822,6 +900,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // draw(grid, coords, EMPTY) of each dying snake's head and body (the tail was
     // handled above): coords = head - prefix sums of the direction deque
     // (core/snake.py:86-94), 64 cells per pass, one dying snake at a time.
+    LSTAMP(43);
     unsigned long long dm = __ballot(isn && death);
     while (dm) {
         const int L = __ffsll((long long)dm) - 1;
@@ -845,6 +924,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     }
     wave_sync();
 
+    LSTAMP(44);
     // fruit respawn (:376-379), one env at a time with the whole wave
     int mtpos_new = mtpos;
     unsigned long long fm = __ballot(live && k == 0 && fruit_taken > 0);
@@ -860,8 +940,8 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         if (g == gg) mtpos_new = mt.pos;
     }
 
+    LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
-    const int dn = !alive;
     if (isn) {
         const double msk = 1.0 - (double)dn;
         s0 = s0 + msk * rew;
@@ -869,12 +949,6 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         s2 = s2 + msk * (counted ? (double)eat : 0.0);
         s3 = s3 + msk * (counted ? (double)kills : 0.0);
     }
-    const int eplen1 = eplen + 1;
-    int fd = ((double)eplen1 >= c.max_steps) ? 1 : dn;
-    const uint32_t done_m = gbits(__ballot(isn && fd));
-    const uint32_t all_m = (1u << S) - 1u;
-    const bool ep_end = !bad && (c.coop ? (done_m != 0u) : (done_m == all_m));
-    if (c.coop && ep_end) fd = 1;
     if (live) {
         o.rew[(int64_t)e * S + k] = rew;
         o.done[(int64_t)e * S + k] = (uint8_t)fd;
@@ -882,10 +956,10 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     if (env_ok && k == 0) {
         o.ep_done[e] = ep_end ? 1 : 0;
         o.err[e] = bad ? 1 : 0;
-        if (ep_end && c.autoreset) {                  // queue the auto-reset
-            const int slot = atomicAdd(&st.resetq[c.N + parity], 1);
-            st.resetq[slot] = e;
-        }
+    }
+    if (qm) {            // queue the auto-resets in the slots claimed above
+        const int base = bcast(qbase, 0);
+        if ((qm >> lane) & 1ull) st.resetq[shard * c.q_cap + base + mbcnt64(qm)] = e;
     }
     int rank = 1;
     for (int j = 0; j < S; j++) rank += (__shfl(s0, gb + j) > s0);
@@ -899,6 +973,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     }
     if (live) { sp[k] = s0; sp[S + k] = s1; sp[2 * S + k] = s2; sp[3 * S + k] = s3; }
 
+    LSTAMP(46);
     // commit the new frames into their ring slots; records; crop centres
     {
         uint4 *dst = reinterpret_cast<uint4 *>(st.grid);
@@ -927,6 +1002,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         nrec.w = ntdir;
         reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + k] = nrec;
     }
+    LSTAMP(47);
 }
 
 // ---------------------------------------------------- step: the observation
@@ -940,11 +1016,16 @@ __global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_stat
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
-    const int R = st.resetq[c.N + parity];
+    // the shard counts, prefix-summed: queue index idx lives in the shard whose
+    // [excl, incl) holds it
+    const int cnt = st.resetq[kQShards * c.q_cap + parity * kQShards + lane];
+    const int incl = wave_scan(cnt, lane), excl = incl - cnt;
+    const int R = bcast(incl, kWave - 1);
     if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
     __builtin_amdgcn_s_setprio(3);
     for (int idx = blockIdx.x; idx < R; idx += gridDim.x) {
-        const int e = st.resetq[idx];
+        const int sh = __ffsll((long long)__ballot(idx >= excl && idx < incl)) - 1;
+        const int e = st.resetq[sh * c.q_cap + idx - bcast(excl, sh)];
         WaveMT mt;
         mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
         if (idx < 128) OBSPROF(idx, lane);
@@ -973,7 +1054,7 @@ __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state s
         org[x * kMaxSnakes + k] = pack_origin(c, p >> 8, p & 255);
     }
     wave_sync();
-    encode(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lane);
+    encode_obs(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lds, lane);
     if (prof_) OBSPROF(384 + (e >> 9), lane);
 }
 

@@ -49,6 +49,30 @@ __global__ void k(unsigned long long *out, int *sink, int seed)
         } else if (P == 6) {               // LDS read dependent chain
             v = (int)lds[(v + it) & 4095] & 7;
             acc += v;
+        } else if (P == 8) {               // 8 dependent SALU adds
+            int x = acc;
+#pragma unroll
+            for (int r = 0; r < 8; r++) { x = x * 3 + it; __asm__ volatile("" : "+s"(x)); }
+            acc = x;
+        } else if (P == 9) {               // 8 dependent VALU ops
+#pragma unroll
+            for (int r = 0; r < 8; r++) { v = v * 3 + it; __asm__ volatile("" : "+v"(v)); }
+        } else if (P == 10) {              // 8 independent VALU ops (4 chains of 2)
+            int a = v, b = v + 1, c2 = v + 2, d = v + 3;
+            a = a * 3 + it; b = b * 5 + it; c2 = c2 * 7 + it; d = d * 9 + it;
+            __asm__ volatile("" : "+v"(a), "+v"(b), "+v"(c2), "+v"(d));
+            a = a * 3 + 1; b = b * 5 + 1; c2 = c2 * 7 + 1; d = d * 9 + 1;
+            __asm__ volatile("" : "+v"(a), "+v"(b), "+v"(c2), "+v"(d));
+            v = a ^ b ^ c2 ^ d;
+        } else if (P == 11) {              // ballot feeding only SALU (no VALU dependency back)
+            m = __ballot(v <= it);
+            acc += __popcll(m);
+            v += 1;
+        } else if (P == 12) {              // VALU op reading SGPR written by SALU each iter
+            acc = acc * 5 + it;
+            __asm__ volatile("" : "+s"(acc));
+            v = v + acc;
+            __asm__ volatile("" : "+v"(v));
         } else if (P == 7) {               // 4 independent ballots + SALU combine (refine-pass shape)
             const unsigned long long a = __ballot(v <= acc), b = __ballot(v <= acc + 5);
             const unsigned long long c = __ballot(v + 1 <= acc), d = __ballot(v + 2 <= acc);
@@ -91,5 +115,10 @@ int main()
     run<5>("ballot -> uniform branch");
     run<6>("dependent ds_read_b32 chain");
     run<7>("4 ballots + SALU combine + 2 mbcnt");
+    run<8>("8 dependent SALU mul-add");
+    run<9>("8 dependent VALU mul-add");
+    run<10>("8 independent VALU mul-add (4 chains)");
+    run<11>("ballot -> SALU only");
+    run<12>("SALU -> VALU reading it");
     return 0;
 }

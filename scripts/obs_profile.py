@@ -25,6 +25,8 @@ def main():
     v = SnakeVecEnv(N, num_snakes=4, seed=0, lib_path=lib, height=20, width=20, snake_length=3, vision_range=5)
     L = ctypes.CDLL(lib)
     L.snake_debug_obsprof.argtypes = [ctypes.c_void_p]
+    L.snake_debug_stamps.argtypes = [ctypes.c_void_p]
+    st = np.zeros(72, dtype=np.uint64)
     buf = np.zeros(512, dtype=np.uint64)
     g = torch.Generator(device='cuda').manual_seed(7)
     acts = torch.randint(0, 3, (300, N, 4), generator=g, device='cuda', dtype=torch.int8)
@@ -37,6 +39,9 @@ def main():
         _, _, done, info = v.step(acts[t])
         torch.cuda.synchronize()
         nres = int(info['episode_done'].sum())
+        L.snake_debug_stamps(st.ctypes.data_as(ctypes.c_void_p))
+        ls = st[40:48].astype(np.int64)
+        logic = {n: int(x - ls[0]) for n, x in zip(('start', 'loaded', 'rules', 'grid', 'dying', 'fruit', 'stats', 'end'), ls)}
         L.snake_debug_obsprof(buf.ctypes.data_as(ctypes.c_void_p))
         b = buf.astype(np.int64)
         rs, re_, es, ee = b[:128], b[128:256], b[256:384], b[384:512]
@@ -47,7 +52,7 @@ def main():
         us = lambda x: (x - t0) / 100.0   # noqa: E731
         pct = lambda x: [round(float(np.percentile(x, p)), 1) for p in (0, 50, 90, 100)]  # noqa: E731
         print(json.dumps({
-            'resets': nres,
+            'resets': nres, 'k_logic_block0_cycles': logic,
             'reset_start_us': pct(us(rs)) if nr else None,
             'reset_dur_us': pct((re_ - rs) / 100.0) if nr else None,
             'reset_end_us': pct(us(re_)) if nr else None,
