@@ -140,6 +140,15 @@ __device__ __forceinline__ int wave_scan(int v, int lane)
 
 __device__ __forceinline__ int bcast(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
+// number of zero bytes of x (exact: no borrow between bytes)
+__device__ __forceinline__ int zero_bytes(uint32_t x)
+{
+    const uint32_t t = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+    return __popc(t);
+}
+
+constexpr int kRespawnT = 4;   // raws per lane prefetched by the fast fruit respawn
+
 __device__ __forceinline__ uint32_t gen_mask(uint32_t m)
 {
     m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
@@ -744,6 +753,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const bool isn = env_ok && k < S;
     uint8_t *work = lds + g * stride;                      // this env's grid being stepped
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + E * stride);
+    // per-env respawn scratch: G * kRespawnT tempered raws, G chosen cells
+    uint32_t *rawbuf = reinterpret_cast<uint32_t *>(lds + E * stride + 2 * kMaxFruits) + g * (G * kRespawnT);
+    uint16_t *cellbuf = reinterpret_cast<uint16_t *>(lds + E * stride + 2 * kMaxFruits + E * G * kRespawnT * 4) + g * G;
     int *qcnt = st.resetq + kQShards * c.q_cap;                       // [2][kQShards]
     if (blockIdx.x == 0) qcnt[(parity ^ 1) * kQShards + lane] = 0;   // next step's counters
     LSTAMP(40);
@@ -773,6 +785,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
                 d4[q] = src[((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)cg * stride) / 16 + off];
         }
     }
+    // keep the statistics loads up here with the others (the compiler would sink
+    // them to their first use, deep in the step, and pay a full memory latency there)
+    __asm__ volatile("" ::"v"(s0), "v"(s1), "v"(s2), "v"(s3));
     const int ncur = (fs == 1) ? 0 : (cur + 1 == fs ? 0 : cur + 1);
     int hr = rec.x & 255, hc = (rec.x >> 8) & 255, tr = (rec.x >> 16) & 255, tc = (rec.x >> 24) & 255;
     int dir = rec.y & 3, alive = (rec.y >> 8) & 1;
@@ -899,35 +914,111 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     wave_sync();
     // draw(grid, coords, EMPTY) of each dying snake's head and body (the tail was
     // handled above): coords = head - prefix sums of the direction deque
-    // (core/snake.py:86-94), 64 cells per pass, one dying snake at a time.
+    // (core/snake.py:86-94). Every dying snake walks its own body on its lane, 16
+    // ring bytes fetched per memory round trip.
     LSTAMP(43);
-    unsigned long long dm = __ballot(isn && death);
-    while (dm) {
-        const int L = __ffsll((long long)dm) - 1;
-        dm &= dm - 1;
-        const int gg = L / G, kk = L - gg * G;
-        const int khr = bcast(hr, L), khc = bcast(hc, L), krh = bcast(rh, L), krl = bcast(rl, L);
-        const uint8_t *kring = st.body + ((int64_t)(e0 + gg) * S + kk) * cap;
-        uint8_t *gw = lds + gg * stride;
-        int br = khr, bc = khc;
-        if (lane == 0) gw[khr * W + khc] = C_EMPTY;
-        for (int m0 = 0; m0 < krl - 1; m0 += kWave) {
-            const int m = m0 + lane;
-            const bool ok = m < krl - 1;
-            const int d = ok ? kring[(krh + m) & (cap - 1)] : 0;
-            const int sr = wave_scan(ok ? dir_dr(d) : 0, lane);
-            const int sc = wave_scan(ok ? dir_dc(d) : 0, lane);
-            if (ok) gw[(br - sr) * W + (bc - sc)] = C_EMPTY;
-            br -= bcast(sr, 63);
-            bc -= bcast(sc, 63);
+    if (isn && death) {
+        const uint8_t *rk = st.body + ((int64_t)e * S + k) * cap;
+        int br = hr, bc = hc;
+        work[br * W + bc] = C_EMPTY;
+        const int n = rl - 1;
+        for (int m0 = 0; m0 < n; m0 += 16) {
+            int d[16];
+#pragma unroll
+            for (int t = 0; t < 16; t++) d[t] = (m0 + t < n) ? rk[(rh + m0 + t) & (cap - 1)] : 0;
+#pragma unroll
+            for (int t = 0; t < 16; t++) {
+                if (m0 + t < n) {
+                    br -= dir_dr(d[t]);
+                    bc -= dir_dc(d[t]);
+                    work[br * W + bc] = C_EMPTY;
+                }
+            }
         }
     }
     wave_sync();
 
     LSTAMP(44);
-    // fruit respawn (:376-379), one env at a time with the whole wave
+    // fruit respawn (:376-379, random_empty_coords grid_util.py:126-133). Fast
+    // path, every env at once on its own G lanes: the draws read the next
+    // G * kRespawnT raw words of the env's key straight from memory (no twist
+    // needed, the key is not rewritten); the empties are counted per lane over a
+    // slice of the grid and the v-th one found by the lane whose slice holds it.
     int mtpos_new = mtpos;
-    unsigned long long fm = __ballot(live && k == 0 && fruit_taken > 0);
+    // per env (all G lanes of the group, snake or not): the empties are counted by all
+    const bool need = env_ok && !bad && fruit_taken > 0;
+    bool fast_done = false;
+    if (__ballot(need)) {
+        const int HW = c.HW, nw = (HW + 3) >> 2, wpl = (nw + G - 1) / G;
+        const int w0 = min(nw, k * wpl), w1 = min(nw, w0 + wpl);
+        const uint32_t *gw = reinterpret_cast<const uint32_t *>(work);
+        int cnt = 0;
+        if (need) {
+            for (int w = w0; w < w1; w++) {
+                uint32_t x = gw[w];
+                if (w == nw - 1 && (HW & 3)) x |= 0xffffffffu << (8 * (HW & 3));   // past the grid
+                cnt += zero_bytes(x);
+            }
+        }
+        const int incl = wave_scan(cnt, lane);
+        const int gbase = __shfl(incl - cnt, gb);
+        const int excl = incl - cnt - gbase;
+        const int Etot = __shfl(incl, gb + G - 1) - gbase;
+        const uint32_t rng = (uint32_t)(Etot - 1), rmask = gen_mask(rng);
+        // rng == 0 draws nothing (randint(0, 1) consumes no raw word)
+        const bool draws = need && Etot > 0 && rng != 0;
+        const bool room = mtpos + G * kRespawnT <= kMtN;
+        uint32_t accm = 0;
+#pragma unroll
+        for (int t = 0; t < kRespawnT; t++) {
+            const int pos = mtpos + t * G + k;
+            const uint32_t raw = (draws && room) ? st.mt[(int64_t)e * kMtN + pos] : 0u;
+            const uint32_t tv = temper(raw) & rmask;
+            rawbuf[t * G + k] = tv;
+            accm |= gbits(__ballot(draws && room && tv <= rng)) << (t * G);
+        }
+        const bool fast = need && Etot > 0 && (!draws || (room && __popc(accm) >= fruit_taken));
+        wave_sync();
+        uint32_t am2 = accm;
+        int used = 0;
+        for (int d = 0; d < MS; d++) {
+            const bool act_d = fast && d < fruit_taken;
+            int v = 0;
+            if (act_d && draws) {
+                const int p = __ffs(am2) - 1;
+                am2 &= am2 - 1u;
+                v = (int)rawbuf[p];
+                used = p + 1;
+            }
+            if (act_d && v >= excl && v < excl + cnt) {      // this lane's slice holds it
+                int need_n = v - excl, x = -1;
+                for (int w = w0; w < w1 && x < 0; w++) {
+                    uint32_t y = gw[w];
+                    if (w == nw - 1 && (HW & 3)) y |= 0xffffffffu << (8 * (HW & 3));
+                    const int z = zero_bytes(y);
+                    if (need_n < z) {
+                        for (int b = 0; b < 4; b++) {
+                            if (((y >> (8 * b)) & 255u) == 0u) {
+                                if (need_n == 0) { x = 4 * w + b; break; }
+                                need_n--;
+                            }
+                        }
+                    } else {
+                        need_n -= z;
+                    }
+                }
+                cellbuf[d] = (uint16_t)x;
+            }
+        }
+        wave_sync();
+        if (fast && k < fruit_taken) work[cellbuf[k]] = C_FRUIT;
+        if (fast && draws) mtpos_new = mtpos + used;
+        fast_done = fast;
+        wave_sync();
+    }
+    // the rest (a twist needed, or too few accepts among the prefetched raws), one
+    // env at a time with the whole wave
+    unsigned long long fm = __ballot(need && !fast_done && k == 0);
     while (fm) {
         const int L = __ffsll((long long)fm) - 1;
         fm &= fm - 1;
@@ -957,10 +1048,12 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         o.ep_done[e] = ep_end ? 1 : 0;
         o.err[e] = bad ? 1 : 0;
     }
+    LSTAMP(48);
     if (qm) {            // queue the auto-resets in the slots claimed above
         const int base = bcast(qbase, 0);
         if ((qm >> lane) & 1ull) st.resetq[shard * c.q_cap + base + mbcnt64(qm)] = e;
     }
+    LSTAMP(49);
     int rank = 1;
     for (int j = 0; j < S; j++) rank += (__shfl(s0, gb + j) > s0);
     if (ep_end) {
@@ -1215,7 +1308,7 @@ int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, con
 {
     const hipStream_t sm = (hipStream_t)stream;
     const int ms = k.S <= 4 ? 4 : (k.S <= 8 ? 8 : 16), epw = kWave / ms;   // envs per k_logic wave
-    const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits;
+    const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits + epw * ms * kRespawnT * 4 + epw * ms * 2;
     const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
     TimedLaunch t1("k_logic", sm);
     if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, k, st, actions, o, parity);

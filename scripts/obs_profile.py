@@ -40,8 +40,9 @@ def main():
         torch.cuda.synchronize()
         nres = int(info['episode_done'].sum())
         L.snake_debug_stamps(st.ctypes.data_as(ctypes.c_void_p))
-        ls = st[40:48].astype(np.int64)
-        logic = {n: int(x - ls[0]) for n, x in zip(('start', 'loaded', 'rules', 'grid', 'dying', 'fruit', 'stats', 'end'), ls)}
+        ls = st[40:50].astype(np.int64)
+        logic = {n: int(x - ls[0]) for n, x in zip(('start', 'loaded', 'rules', 'grid', 'dying', 'fruit', 'stats', 'end',
+                                                    'outputs', 'queued'), ls)}
         L.snake_debug_obsprof(buf.ctypes.data_as(ctypes.c_void_p))
         b = buf.astype(np.int64)
         rs, re_, es, ee = b[:128], b[128:256], b[256:384], b[384:512]
