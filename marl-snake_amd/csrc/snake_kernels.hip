@@ -284,10 +284,14 @@ __device__ uint32_t mt_draw(WaveMT &m, uint32_t mask, uint32_t rng, int lane)
     }
 }
 
-__device__ __forceinline__ int mbcnt64(unsigned long long x)
+// set bits of x below this lane, + add
+__device__ __forceinline__ int mbcnt64(unsigned long long x, int add = 0)
 {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(x >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)x, 0u));
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(x >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)x, (uint32_t)add));
 }
+
+// this lane's bit of a wave mask, as a lane predicate (v_cndmask on the SGPR pair)
+__device__ __forceinline__ bool inv_ballot(unsigned long long m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 
 // permutation(n) = shuffle(arange(n)) draws j_i = random_interval(i) for
 // i = n-1 .. 1 (snake_env.py:581). Only arr[0..S) is ever used, so instead of the
@@ -353,26 +357,26 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
             tw1 = b;
             qc = q;
         }
-        const int p0 = lane - l0, p1 = 64 + lane - l0;
+        const int p0 = lane - l0;   // stream offset of this lane's first word (second: + 64)
         // words before the stream position or past the key never accept: give them
         // an impossible value instead of masking every ballot
         const int w0 = p0 >= 0 ? (int)(tw0 & mask) : INT_MAX;
-        const int w1 = (p1 >= 0 && base + 64 + lane < kMtN) ? (int)(tw1 & mask) : INT_MAX;
-        bool acc0 = w0 <= i - p0, acc1 = w1 <= i - p1;
-        unsigned long long a0 = __ballot(acc0), a1 = __ballot(acc1);
+        const int w1 = (p0 >= -64 && base + 64 + lane < kMtN) ? (int)(tw1 & mask) : INT_MAX;
+        // a = sure accepts (upper bound: the offset), c = possible accepts (lower: 0)
+        unsigned long long a0 = __ballot(w0 <= i - p0), a1 = __ballot(w1 <= i - 64 - p0);
         unsigned long long c0 = __ballot(w0 <= i), c1 = __ballot(w1 <= i);
         const unsigned long long r2_ = RNOW();
         COUNT_ADD(4, r2_ - r0_);
-        while ((a0 ^ c0) | (a1 ^ c1)) {
+        unsigned long long und = (a0 ^ c0) | (a1 ^ c1);
+        while (und) {
             COUNT_ADD(3, 1);
             const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
-            const int L1 = __popcll(a0) + mbcnt64(a1), U1 = __popcll(c0) + mbcnt64(c1);
-            acc0 = w0 <= i - U0;
-            acc1 = w1 <= i - U1;
+            const int L1 = mbcnt64(a1, __popcll(a0)), U1 = mbcnt64(c1, __popcll(c0));
+            a0 = __ballot(w0 <= i - U0);
+            a1 = __ballot(w1 <= i - U1);
             c0 = __ballot(w0 <= i - L0);
             c1 = __ballot(w1 <= i - L1);
-            a0 = __ballot(acc0);
-            a1 = __ballot(acc1);
+            und = (a0 ^ c0) | (a1 ^ c1);
         }
         const unsigned long long r3_ = RNOW();
         COUNT_ADD(5, r3_ - r2_);
@@ -382,30 +386,31 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
         const int k = i - lo + 1;  // accepts left in this bracket
         if (A >= k) {
             if (A0 >= k) {
-                const int b = __ffsll((long long)__ballot(acc0 && mbcnt64(a0) == k - 1)) - 1;
-                acc0 = acc0 && lane <= b;
-                acc1 = false;
+                const int b = __ffsll((long long)__ballot(inv_ballot(a0) && mbcnt64(a0) == k - 1)) - 1;
                 a0 &= (2ull << b) - 1ull;
                 a1 = 0;
                 A0 = k;
                 end = b + 1;
             } else {
                 const int k1 = k - A0;
-                const int b = __ffsll((long long)__ballot(acc1 && mbcnt64(a1) == k1 - 1)) - 1;
-                acc1 = acc1 && lane <= b;
+                const int b = __ffsll((long long)__ballot(inv_ballot(a1) && mbcnt64(a1) == k1 - 1)) - 1;
                 a1 &= (2ull << b) - 1ull;
                 end = 64 + b + 1;
             }
             A = k;
         }
-        const int ii0 = i - mbcnt64(a0), ii1 = i - A0 - mbcnt64(a1);
+        const int ii0 = i - mbcnt64(a0), ii1 = (i - A0) - mbcnt64(a1);
+#ifdef SNAKE_DB_NOREC
+        if (false) {
+#else
         if (i - A + 1 >= S) {
+#endif
             // every index of the round >= S: unconditional ds_min, misses to the dummy
-            link_min((acc0 && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
-            link_min((acc1 && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
+            link_min((inv_ballot(a0) && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
+            link_min((inv_ballot(a1) && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
         } else {
-            if (acc0) perm_record(ii0, w0, S, link, jsmall);
-            if (acc1) perm_record(ii1, w1, S, link, jsmall);
+            if (inv_ballot(a0)) perm_record(ii0, w0, S, link, jsmall);
+            if (inv_ballot(a1)) perm_record(ii1, w1, S, link, jsmall);
         }
         m.pos = base + end;
         i -= A;
@@ -1394,6 +1399,34 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
     if (it != snake::g_done.end()) snake::g_done.erase(it);
     return SNAKE_OK;
 }
+
+#if defined(SNAKE_STAMPS) || defined(SNAKE_DRAWBENCH)
+// Isolated draw benchmark: one permutation's draws on one wave, outside the
+// reset kernel's register pressure (cycles, final MT position).
+__global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsigned long long *out)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    snake::lu32 *link = (snake::lu32 *)lds;
+    snake::lu16 *jsmall = (snake::lu16 *)(lds + 4 * (n + 64 + 4));
+    for (int x = lane; x < n + 64; x += 64) link[x] = 0xffffffffu;
+    snake::WaveMT mt;
+    snake::mt_load(mt, mt_src, pos0, lane);
+    snake::wave_sync();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    snake::mt_perm_draws(mt, n, S, link, n, jsmall, lane);
+    snake::wave_sync();
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { out[0] = t1 - t0; out[1] = (unsigned long long)mt.pos; }
+}
+
+extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, int S, unsigned long long *out_dev)
+{
+    hipLaunchKernelGGL(k_drawbench, dim3(1), dim3(64), 4 * (n + 64 + 4) + 64, 0, mt_dev, pos0, n, S, out_dev);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+#endif
 
 #ifdef SNAKE_STAMPS
 extern "C" int snake_debug_obsprof(unsigned long long *out /* 512 */)
