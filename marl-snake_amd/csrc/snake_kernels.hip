@@ -313,6 +313,72 @@ __device__ __forceinline__ void perm_record(int ii, int w, int S, NP *link, lu16
     else if (w != ii) link_min(link + w, (uint32_t)ii);
 }
 
+// One draw round over the unread words of the register pair (tw0, tw1) at key
+// offset base (see mt_perm_draws).
+template <typename NP>
+__device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base, WaveMT &m, int &i,
+                                           uint32_t &mask, int &lo, int S, NP *link, NP *dummy,
+                                           lu16 *jsmall, int lane)
+{
+    const int l0 = m.pos - base;
+    const int p0 = lane - l0;   // stream offset of this lane's first word (second: + 64)
+    // words before the stream position or past the key never accept: give them
+    // an impossible value instead of masking every ballot
+    const int w0 = p0 >= 0 ? (int)(tw0 & mask) : INT_MAX;
+    const int w1 = (p0 >= -64 && base + 64 + lane < kMtN) ? (int)(tw1 & mask) : INT_MAX;
+    // a = sure accepts (upper bound: the offset), c = possible accepts (lower: 0)
+    unsigned long long a0 = __ballot(w0 <= i - p0), a1 = __ballot(w1 <= i - 64 - p0);
+    unsigned long long c0 = __ballot(w0 <= i), c1 = __ballot(w1 <= i);
+    unsigned long long und = (a0 ^ c0) | (a1 ^ c1);
+    while (und) {
+        const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
+        const int L1 = mbcnt64(a1, __popcll(a0)), U1 = mbcnt64(c1, __popcll(c0));
+        a0 = __ballot(w0 <= i - U0);
+        a1 = __ballot(w1 <= i - U1);
+        c0 = __ballot(w0 <= i - L0);
+        c1 = __ballot(w1 <= i - L1);
+        und = (a0 ^ c0) | (a1 ^ c1);
+    }
+    int A0 = __popcll(a0);
+    int A = A0 + __popcll(a1);
+    int end = min(128, kMtN - base);
+    const int k = i - lo + 1;  // accepts left in this bracket
+    if (A >= k) {
+        if (A0 >= k) {
+            const int b = __ffsll((long long)__ballot(inv_ballot(a0) && mbcnt64(a0) == k - 1)) - 1;
+            a0 &= (2ull << b) - 1ull;
+            a1 = 0;
+            A0 = k;
+            end = b + 1;
+        } else {
+            const int k1 = k - A0;
+            const int b = __ffsll((long long)__ballot(inv_ballot(a1) && mbcnt64(a1) == k1 - 1)) - 1;
+            a1 &= (2ull << b) - 1ull;
+            end = 64 + b + 1;
+        }
+        A = k;
+    }
+    const int ii0 = i - mbcnt64(a0), ii1 = (i - A0) - mbcnt64(a1);
+#ifdef SNAKE_DB_NOREC
+    if (false) {
+#else
+    if (i - A + 1 >= S) {
+#endif
+        // every index of the round >= S: unconditional ds_min, misses to the dummy
+        link_min((inv_ballot(a0) && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
+        link_min((inv_ballot(a1) && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
+    } else {
+        if (inv_ballot(a0)) perm_record(ii0, w0, S, link, jsmall);
+        if (inv_ballot(a1)) perm_record(ii1, w1, S, link, jsmall);
+    }
+    m.pos = base + end;
+    i -= A;
+    if (i < lo && i >= 1) {
+        mask = gen_mask((uint32_t)i);
+        lo = (int)(mask >> 1) + 1;
+    }
+}
+
 template <typename NP>
 __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, int lane,
                               int e = -1)
@@ -322,103 +388,29 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
     COUNT_DECL;
     uint32_t mask = gen_mask((uint32_t)i);
     int lo = (int)(mask >> 1) + 1;
-    // lanes with nothing to record write their own dummy entry past the table
-    NP *dummy = link + link_n + lane;
     // the tempered key stays in registers: the rounds never read LDS, so nothing
-    // waits for the link-table atomics until the draws are done
+    // waits for the link-table atomics until the draws are done. The rounds of a
+    // key block run pair by pair, unrolled: each pair's words are fixed registers.
     uint32_t tk[10];
 #pragma unroll
     for (int t = 0; t < 10; t++) tk[t] = temper(m.w[t]);
-    int qc = -1;
-    uint32_t tw0 = 0, tw1 = 0;
-    while (i >= 1) {
+    NP *dummy = link + link_n + lane;   // lanes with nothing to record hit their own dummy
+    // every round advances the stream; the cap only guarantees that a broken
+    // invariant ends the wave instead of hanging the GPU
+    for (int guard = 0; i >= 1 && guard < (1 << 20); guard++) {
         if (m.pos >= kMtN) {
-            const unsigned long long t0_ = NOW();
             mt_twist(m, lane);
 #pragma unroll
             for (int t = 0; t < 10; t++) tk[t] = temper(m.w[t]);
-            qc = -1;
             COUNT(e, lane, 0);
-            COUNT_ADD(2, NOW() - t0_);
         }
-        const unsigned long long r0_ = RNOW();
-        COUNT(e, lane, 1);
-        const int q = m.pos >> 7, l0 = m.pos & 127;
-        const int base = q << 7;
-        if (q != qc) {
-            uint32_t a = 0, b = 0;
 #pragma unroll
-            for (int r = 0; r < 5; r++) {
-                const uint32_t sel = 0u - (uint32_t)(q == r);
-                a |= tk[2 * r] & sel;
-                b |= tk[2 * r + 1] & sel;
+        for (int q = 0; q < 5; q++) {
+            while (i >= 1 && m.pos < kMtN && (m.pos >> 7) == q) {
+                COUNT(e, lane, 1);
+                draw_round(tk[2 * q], tk[2 * q + 1], q << 7, m, i, mask, lo, S, link, dummy, jsmall, lane);
             }
-            tw0 = a;
-            tw1 = b;
-            qc = q;
         }
-        const int p0 = lane - l0;   // stream offset of this lane's first word (second: + 64)
-        // words before the stream position or past the key never accept: give them
-        // an impossible value instead of masking every ballot
-        const int w0 = p0 >= 0 ? (int)(tw0 & mask) : INT_MAX;
-        const int w1 = (p0 >= -64 && base + 64 + lane < kMtN) ? (int)(tw1 & mask) : INT_MAX;
-        // a = sure accepts (upper bound: the offset), c = possible accepts (lower: 0)
-        unsigned long long a0 = __ballot(w0 <= i - p0), a1 = __ballot(w1 <= i - 64 - p0);
-        unsigned long long c0 = __ballot(w0 <= i), c1 = __ballot(w1 <= i);
-        const unsigned long long r2_ = RNOW();
-        COUNT_ADD(4, r2_ - r0_);
-        unsigned long long und = (a0 ^ c0) | (a1 ^ c1);
-        while (und) {
-            COUNT_ADD(3, 1);
-            const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
-            const int L1 = mbcnt64(a1, __popcll(a0)), U1 = mbcnt64(c1, __popcll(c0));
-            a0 = __ballot(w0 <= i - U0);
-            a1 = __ballot(w1 <= i - U1);
-            c0 = __ballot(w0 <= i - L0);
-            c1 = __ballot(w1 <= i - L1);
-            und = (a0 ^ c0) | (a1 ^ c1);
-        }
-        const unsigned long long r3_ = RNOW();
-        COUNT_ADD(5, r3_ - r2_);
-        int A0 = __popcll(a0);
-        int A = A0 + __popcll(a1);
-        int end = min(128, kMtN - base);
-        const int k = i - lo + 1;  // accepts left in this bracket
-        if (A >= k) {
-            if (A0 >= k) {
-                const int b = __ffsll((long long)__ballot(inv_ballot(a0) && mbcnt64(a0) == k - 1)) - 1;
-                a0 &= (2ull << b) - 1ull;
-                a1 = 0;
-                A0 = k;
-                end = b + 1;
-            } else {
-                const int k1 = k - A0;
-                const int b = __ffsll((long long)__ballot(inv_ballot(a1) && mbcnt64(a1) == k1 - 1)) - 1;
-                a1 &= (2ull << b) - 1ull;
-                end = 64 + b + 1;
-            }
-            A = k;
-        }
-        const int ii0 = i - mbcnt64(a0), ii1 = (i - A0) - mbcnt64(a1);
-#ifdef SNAKE_DB_NOREC
-        if (false) {
-#else
-        if (i - A + 1 >= S) {
-#endif
-            // every index of the round >= S: unconditional ds_min, misses to the dummy
-            link_min((inv_ballot(a0) && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
-            link_min((inv_ballot(a1) && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
-        } else {
-            if (inv_ballot(a0)) perm_record(ii0, w0, S, link, jsmall);
-            if (inv_ballot(a1)) perm_record(ii1, w1, S, link, jsmall);
-        }
-        m.pos = base + end;
-        i -= A;
-        if (i < lo && i >= 1) {
-            mask = gen_mask((uint32_t)i);
-            lo = (int)(mask >> 1) + 1;
-        }
-        COUNT_ADD(6, RNOW() - r3_);
     }
     COUNT_FLUSH(e, lane);
 }

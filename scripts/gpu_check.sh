@@ -19,8 +19,8 @@ for s in "$@"; do
     case $s in
         build) step build 300 python -c "import __graft_entry__ as g; g.build()" ;;
         smoke) step smoke 300 python __graft_entry__.py smoke ;;
-        tests) step tests 900 python -m pytest tests -x -q -m gpu ;;
-        testsv) step tests 900 python -m pytest tests -q -m gpu -rf ;;
+        tests) step tests 300 python -m pytest tests -x -q -m gpu ;;
+        testsv) step tests 300 python -m pytest tests -q -m gpu -rf ;;
         bench) step bench 600 python bench.py ;;
         benchq) step bench 300 python bench.py --steps 200 --warmup 50 --cpu-seconds 5 ;;
         benchnt) step benchnt 300 python bench.py --timing-stride 0 --no-cpu-baseline ;;
