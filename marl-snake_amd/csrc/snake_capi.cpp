@@ -273,6 +273,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         const uint64_t fsoh = (uint64_t)k->fs * k->oh, oh = (uint64_t)k->oh;
         k->mag_fsoh = (uint32_t)(((1ull << 32) + fsoh - 1) / fsoh);
         k->mag_oh = (uint32_t)(((1ull << 32) + oh - 1) / oh);
+        k->mag_W = (uint32_t)(((1ull << 32) + k->W - 1) / k->W);
     }
     k->link_stride = (int)round_up(k->n_cand, 4) + kWave;
     k->link_in_lds = 4 * k->link_stride <= kLinkLdsMax;

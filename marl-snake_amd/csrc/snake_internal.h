@@ -39,6 +39,7 @@ struct KCfg {
     // fs*oh and oh (x / d == umulhi(x, m) for the row indices used)
     int enc_group, lds_stage;
     uint32_t mag_fsoh, mag_oh;
+    uint32_t mag_W;             // x / W == umulhi(x, mag_W) for cell indices x < H*W
     int reset_slots;            // min(N, kResetSlots)
     int q_envs_per_block;       // envs per k_logic block (64 / MS)
     int q_cap;                  // queue entries per shard

@@ -329,7 +329,10 @@ __device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base,
     // a = sure accepts (upper bound: the offset), c = possible accepts (lower: 0)
     unsigned long long a0 = __ballot(w0 <= i - p0), a1 = __ballot(w1 <= i - 64 - p0);
     unsigned long long c0 = __ballot(w0 <= i), c1 = __ballot(w1 <= i);
+    // (the empty asm keeps the test on the OR of both halves: folded into two
+    // mask compares, it costs a bool materialisation per pass)
     unsigned long long und = (a0 ^ c0) | (a1 ^ c1);
+    __asm__ volatile("" : "+s"(und));
     while (und) {
         const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
         const int L1 = mbcnt64(a1, __popcll(a0)), U1 = mbcnt64(c1, __popcll(c0));
@@ -338,6 +341,7 @@ __device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base,
         c0 = __ballot(w0 <= i - L0);
         c1 = __ballot(w1 <= i - L1);
         und = (a0 ^ c0) | (a1 ^ c1);
+        __asm__ volatile("" : "+s"(und));
     }
     int A0 = __popcll(a0);
     int A = A0 + __popcll(a1);
@@ -359,21 +363,17 @@ __device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base,
         A = k;
     }
     const int ii0 = i - mbcnt64(a0), ii1 = (i - A0) - mbcnt64(a1);
-#ifdef SNAKE_DB_NOREC
-    if (false) {
-#else
-    if (i - A + 1 >= S) {
-#endif
+    if (__builtin_expect(i - A + 1 < S, 0)) {   // the last rounds: some indices < S
+        if (inv_ballot(a0)) perm_record(ii0, w0, S, link, jsmall);
+        if (inv_ballot(a1)) perm_record(ii1, w1, S, link, jsmall);
+    } else {
         // every index of the round >= S: unconditional ds_min, misses to the dummy
         link_min((inv_ballot(a0) && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
         link_min((inv_ballot(a1) && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
-    } else {
-        if (inv_ballot(a0)) perm_record(ii0, w0, S, link, jsmall);
-        if (inv_ballot(a1)) perm_record(ii1, w1, S, link, jsmall);
     }
     m.pos = base + end;
     i -= A;
-    if (i < lo && i >= 1) {
+    if (i < lo) {          // next power-of-two bracket (i < 1 ends the draws anyway)
         mask = gen_mask((uint32_t)i);
         lo = (int)(mask >> 1) + 1;
     }
@@ -651,7 +651,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     }
     // make_grid (grid_util.py:14-20), then paint (:138-144)
     for (int x = lane; x < c.HW; x += kWave) {
-        const int r = x / W, cc = x - r * W;
+        const int r = (int)__umulhi((uint32_t)x, c.mag_W), cc = x - r * W;   // x / W
         work[x] = (r == 0 || cc == 0 || r == c.H - 1 || cc == W - 1) ? C_WALL : C_EMPTY;
     }
     wave_sync();
@@ -664,7 +664,8 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         uint8_t *ring = st.body + ((int64_t)e * S + sk) * c.ring_cap;
         if (si < L - 1) ring[si] = (uint8_t)dir_of_diff(cell - nxt, W);
         if (si == 0) {
-            const int hr = cell / W, hc = cell - hr * W, tr = tailcell / W, tc = tailcell - tr * W;
+            const int hr = (int)__umulhi((uint32_t)cell, c.mag_W), hc = cell - hr * W;
+            const int tr = (int)__umulhi((uint32_t)tailcell, c.mag_W), tc = tailcell - tr * W;
             int4 rec;
             rec.x = hr | (hc << 8) | (tr << 16) | (tc << 24);
             rec.y = dir_of_diff(cell - nxt, W) | (1 << 8);
