@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 5
+#define SNAKE_ABI_VERSION 6
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -126,6 +126,16 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
  * stream the library keeps per caller stream; joined before the call returns. */
 int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
                const int8_t *actions, const snake_out *out, void *stream);
+
+/* RGB image of every env's current grid: rgb_from_grid(grid, Cell, CellColors)
+ * (grid_util.py:164-175), the frame of SnakeEnv.render('rgb_array') and of the
+ * 'gif' frames via image_from_grid (snake_env.py:284-293). palette is HOST
+ * memory, uint8 [6][16][3]: the colour of a cell of code v % 10 owned by snake
+ * v / 10, i.e. CellColors[code][id % len] * 0.7 ** (id // len) truncated to
+ * uint8 (snake.py:14-30), precomputed by the caller with the reference's own
+ * arithmetic. rgb is device uint8 [N][H][W][3]. */
+int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
+                     const uint8_t *palette, uint8_t *rgb, void *stream);
 
 /* Profiling aid. While enabled, every kernel launch of snake_step / snake_reset
  * is bracketed by timing events on its own stream. snake_timing_read returns the

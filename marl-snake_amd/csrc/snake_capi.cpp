@@ -408,4 +408,16 @@ int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, co
     return launch_step(k, *st, actions, *out, (int)parity, stream);
 }
 
+int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
+                     const uint8_t *palette, uint8_t *rgb, void *stream)
+{
+    KCfg k;
+    int rc = build_kcfg(cfg, num_envs, n_cand_of(cfg), &k);
+    if (rc) return rc;
+    if (!st || !st->grid || !st->env) { set_error("snake_state.grid/env is NULL"); return SNAKE_E_ARG; }
+    if (!palette) { set_error("palette is NULL"); return SNAKE_E_ARG; }
+    if (!rgb) { set_error("rgb is NULL"); return SNAKE_E_ARG; }
+    return launch_render(k, *st, palette, rgb, stream);
+}
+
 }  // extern "C"

@@ -57,5 +57,7 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
                  void *stream);
 int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, const snake_out &o,
                 int parity, void *stream);
+int launch_render(const KCfg &k, const snake_state &st, const uint8_t *palette, uint8_t *rgb,
+                  void *stream);
 
 }  // namespace snake

@@ -1181,6 +1181,51 @@ __global__ void k_seed(const KCfg c, const snake_state st, uint32_t base, long l
     st.env[(int64_t)e * kEnvRec + ENV_MTPOS] = kMtN;
 }
 
+// rgb_from_grid (grid_util.py:164-175) of every env's current grid: a palette
+// lookup per cell. Each thread writes 4 consecutive cells of the flat
+// [N][H][W] image as three 4-byte stores (12 bytes at a 12-byte offset; cells
+// past the last whole quad go byte by byte). HBM-bound: reads one
+// ring byte and writes 3 bytes per cell, plus the 4-byte cur index per env.
+struct RenderPal {
+    uint8_t rgb[6 * kMaxSnakes * 3];
+};
+
+__device__ __forceinline__ uint32_t render_cell(const KCfg &c, const snake_state &st,
+                                                const RenderPal &pal, long long x)
+{
+    const long long e = x / c.HW;
+    const int cell = (int)(x - e * c.HW);
+    const int cur = st.env[e * kEnvRec + ENV_CUR];
+    const int v = st.grid[e * c.ring_bytes + (long long)cur * c.grid_stride + cell];
+    const int code = v % 10, id = v / 10;
+    if (code > 5 || id >= kMaxSnakes) return 0u;   // not a reachable grid value
+    const uint8_t *p = pal.rgb + (code * kMaxSnakes + id) * 3;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+}
+
+__global__ void k_render(const KCfg c, const snake_state st, const RenderPal pal, uint8_t *rgb)
+{
+    const long long total = (long long)c.N * c.HW;
+    const long long x0 = 4ll * ((long long)blockIdx.x * blockDim.x + threadIdx.x);
+    if (x0 >= total) return;
+    if (x0 + 4 <= total) {
+        uint32_t q[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) q[t] = render_cell(c, st, pal, x0 + t);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(rgb + 3 * x0);
+        dst[0] = q[0] | (q[1] << 24);
+        dst[1] = (q[1] >> 8) | (q[2] << 16);
+        dst[2] = (q[2] >> 16) | (q[3] << 8);
+    } else {
+        for (long long x = x0; x < x0 + 4 && x < total; x++) {
+            const uint32_t q = render_cell(c, st, pal, x);
+            rgb[3 * x] = (uint8_t)q;
+            rgb[3 * x + 1] = (uint8_t)(q >> 8);
+            rgb[3 * x + 2] = (uint8_t)(q >> 16);
+        }
+    }
+}
+
 // ------------------------------------------------------------- kernel timing
 // Profiling aid (snake_timing_enable / snake_timing_read): pairs of timing events
 // around each launch, resolved when read. Event objects are pooled.
@@ -1255,6 +1300,19 @@ int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_
     hipLaunchKernelGGL(k_seed, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, k, st,
                        base_seed, (long long)env_offset);
     return check_launch("k_seed");
+}
+
+int launch_render(const KCfg &k, const snake_state &st, const uint8_t *palette, uint8_t *rgb,
+                  void *stream)
+{
+    RenderPal pal;
+    memcpy(pal.rgb, palette, sizeof(pal.rgb));
+    const long long quads = ((long long)k.N * k.HW + 3) / 4;
+    const int threads = 256;
+    const long long blocks = (quads + threads - 1) / threads;
+    hipLaunchKernelGGL(k_render, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream, k, st,
+                       pal, rgb);
+    return check_launch("k_render");
 }
 
 int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, const snake_out &o,

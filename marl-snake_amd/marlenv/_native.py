@@ -10,11 +10,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 5
+SNAKE_ABI_VERSION = 6
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
-           'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version')
+           'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version')
 
 
 class SnakeCfg(ctypes.Structure):
@@ -80,6 +80,7 @@ def lib(path=None):
                               ctypes.POINTER(SnakeOut), P]
     L.snake_step.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P,
                              ctypes.POINTER(SnakeOut), P]
+    L.snake_render_rgb.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P, P, P]
     L.snake_timing_enable.argtypes = [ctypes.c_int]
     L.snake_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_int64)]

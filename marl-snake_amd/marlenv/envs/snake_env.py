@@ -21,6 +21,10 @@ Deviation: on an invalid action the reference raises KeyError after having
 already turned the lower-index snakes; here KeyError is raised with the env
 untouched.
 """
+import datetime
+import os
+import warnings
+
 import numpy as np
 
 from .. import spaces
@@ -52,6 +56,7 @@ class SnakeEnv:
         self.num_snakes = num_snakes
         self.num_fruits = m['num_fruits']
         self.grid_shape = (height, width)
+        self.frame_buffer = []
         self.snake_length = snake_length
         self.vision_range = vision_range
         self.observer = observer
@@ -97,6 +102,7 @@ class SnakeEnv:
         obs = self._vec.reset()
         out = obs[0].cpu().numpy()
         self._pull_rng()
+        self.frame_buffer = []
         return np.array(out, dtype=np.uint8)
 
     def seed(self, seed=42):
@@ -168,10 +174,36 @@ class SnakeEnv:
         return int(self._vec.episode_lengths()[0].item())
 
     def render(self, mode='ascii'):
-        if mode != 'ascii':
-            raise NotImplementedError('only ascii render is provided (visualisation is out of scope)')
-        sym = {0: '.', 1: '#', 2: 'o', 3: 'H', 4: 'b', 5: 't'}
-        print('\n'.join(''.join(sym[v % 10] for v in row) for row in self.grid))
+        """SnakeEnv.render (snake_env.py:267-296): 'ascii' prints the grid,
+        'rgb_array' returns rgb_from_grid of it (H, W, 3) uint8, 'gif' appends
+        image_from_grid's PIL frame to frame_buffer (save_gif writes them),
+        'human' does nothing. The RGB frame comes from the device (k_render)."""
+        if mode == 'ascii':
+            sym = {0: '.', 1: '#', 2: 'o', 3: 'H', 4: 'b', 5: 't'}
+            print('\n'.join(''.join(sym[v % 10] for v in row) for row in self.grid))
+        elif mode == 'rgb_array':
+            return self._vec.render_rgb()[0].cpu().numpy()
+        elif mode == 'gif':
+            from PIL import Image
+            from ..core.render import upscale
+            rgb = self._vec.render_rgb()[0].cpu().numpy()
+            self.frame_buffer.append(Image.fromarray(upscale(rgb), 'RGB'))
+        elif mode == 'human':
+            pass
+
+    def save_gif(self, fp=None):
+        """SnakeEnv.save_gif (snake_env.py:419-437)."""
+        if fp is None:
+            save_dir = os.path.join(os.getcwd(), 'tmp')
+            fp = os.path.join(save_dir, '{}.gif'.format(datetime.datetime.now().strftime('%Y%m%d%H%M%S')))
+            os.makedirs(save_dir, exist_ok=True)
+        if not self.frame_buffer:
+            warnings.warn("You must call render('gif') first. No images to save.")
+        else:
+            print('Saving image to {}'.format(fp))
+            self.frame_buffer[0].save(fp, save_all=True, append_images=self.frame_buffer[1:],
+                                      format='GIF', loop=0)
+        return fp
 
     def close(self):
         pass

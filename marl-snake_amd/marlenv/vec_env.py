@@ -85,6 +85,7 @@ class SnakeVecEnv:
         self.observation_space = spaces.Box(0, 255, (N,) + self.obs_shape, np.uint8)
         self.action_space = spaces.Box(0, self.action_n - 1, (N, S), np.int64)
         self._reset_done = False
+        self._palette = None
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
@@ -161,16 +162,31 @@ class SnakeVecEnv:
             raise KeyError(f'invalid action for an alive snake in envs {bad[:8]}')
         return out['obs'], out['rew'], out['done'], info
 
+    def render_rgb(self):
+        """rgb_from_grid of every env's current grid (grid_util.py:164-175), on the
+        device: (N, H, W, 3) uint8, freshly allocated (kernel k_render)."""
+        torch = _torch()
+        H, W = self.grid_shape
+        rgb = torch.empty((self.num_envs, H, W, 3), dtype=torch.uint8, device=self.device)
+        if self._palette is None:
+            from .core.render import palette
+            self._palette = np.ascontiguousarray(palette())
+        check(self._L.snake_render_rgb(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+                                       self._palette.ctypes.data_as(ctypes.c_void_p),
+                                       ctypes.c_void_p(rgb.data_ptr()), self._stream()))
+        return rgb
+
     # --------------------------------------------------------- introspection
     def grids(self):
-        """Current grid of every env, (N, H, W) int8 (newest ring slot)."""
+        """Current grid of every env, (N, H, W) uint8 cell values 10*idx + code
+        (newest ring slot)."""
         torch = _torch()
         lay, fs = self.layout, self.cfg.frame_stack
         H, W = self.grid_shape
         ring = self.grid.view(self.num_envs, fs, lay.grid_stride)
         cur = self.env_rec.view(self.num_envs, 8)[:, 2].long()
         g = ring[torch.arange(self.num_envs, device=self.device), cur][:, :H * W]
-        return g.reshape(self.num_envs, H, W).view(torch.int8)
+        return g.reshape(self.num_envs, H, W)
 
     def alive_counters(self):
         return self.env_rec.view(self.num_envs, 8)[:, 0]

@@ -648,9 +648,9 @@ int so_step(so_env *e, const int32_t *actions, uint8_t *obs, double *rews, uint8
     return 1;
 }
 
-void so_get_grid(const so_env *e, int8_t *out)
+void so_get_grid(const so_env *e, uint8_t *out)
 {
-    for (int i = 0; i < e->H * e->W; i++) out[i] = (int8_t)e->grid[i];
+    for (int i = 0; i < e->H * e->W; i++) out[i] = (uint8_t)e->grid[i];   /* <= 155 for S <= 16 */
 }
 
 int64_t so_alive_snakes(const so_env *e) { return e->alive_snakes; }

@@ -49,7 +49,7 @@ int     so_reset(so_env *e, uint8_t *obs);             /* snake_env.py:131-159 *
  * -1 on an invalid action for an alive snake (the reference's KeyError). */
 int     so_step(so_env *e, const int32_t *actions, uint8_t *obs, double *rews,
                 uint8_t *dones, so_info *info);
-void    so_get_grid(const so_env *e, int8_t *out);     /* H*W */
+void    so_get_grid(const so_env *e, uint8_t *out);     /* H*W */
 int64_t so_alive_snakes(const so_env *e);
 int64_t so_episode_length(const so_env *e);
 /* per snake: head r,c, tail r,c, dir (0 UP,1 RIGHT,2 DOWN,3 LEFT), alive, length(cells) */

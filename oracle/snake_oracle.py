@@ -136,7 +136,7 @@ class OracleEnv:
 
     @property
     def grid(self):
-        g = np.zeros((self.H, self.W), np.int8)
+        g = np.zeros((self.H, self.W), np.uint8)
         lib().so_get_grid(self._h, _ptr(g))
         return g
 
@@ -191,3 +191,27 @@ def candidates(H, W, L):
     out = np.zeros((n, L, 2), np.int16)
     lib().so_candidates(H, W, L, _ptr(out))
     return out
+
+
+# ------------------------------------------------------------------ rendering
+# CellColors (marlenv/marlenv/core/snake.py:14-30), restated for the checker.
+_WHEEL = [(104, 255, 0), (255, 191, 0), (255, 0, 92), (0, 111, 255)]
+_HEAD_WHEEL = [tuple(min(255, int(x * 2.0)) for x in rgb) for rgb in _WHEEL]
+CELL_COLORS = {0: [(0, 0, 0)], 1: [(32, 32, 32)], 2: [(223, 7, 22)],
+               3: _HEAD_WHEEL, 4: _WHEEL, 5: _WHEEL}
+
+
+def rgb_from_grid(grid):
+    """rgb_from_grid(grid, Cell, CellColors) (grid_util.py:164-175): per cell,
+    colour list of code v % 10, entry (v // 10) % len, times 0.7 ** cycle with
+    cycle = (v // 10) // len, truncated to uint8. Cell-by-cell, as the reference."""
+    grid = np.asarray(grid)
+    rgb = np.zeros((*grid.shape, 3), dtype=np.uint8)
+    for r in range(grid.shape[0]):
+        for c in range(grid.shape[1]):
+            v = int(grid[r, c])
+            colors = CELL_COLORS[v % 10]
+            cell_id = v // 10
+            color = np.array(colors[cell_id % len(colors)])
+            rgb[r, c] = (color * 0.7**(cell_id // len(colors))).astype(np.uint8)
+    return rgb

@@ -273,3 +273,42 @@ def test_make_snake_surface():
     assert pv['num_envs'] == 64
     ob = venv.reset()
     assert tuple(ob.shape) == (64, 4, 11, 11, 8) and ob.is_cuda
+
+
+@pytest.mark.parametrize('S,kw', [(4, dict(height=20, width=20, vision_range=5)),
+                                  (16, dict(height=24, width=24, snake_length=2, vision_range=3)),
+                                  (3, dict(height=9, width=7, snake_length=2))])
+def test_render_rgb_matches_oracle(S, kw):
+    """k_render (snake_render_rgb) == rgb_from_grid (grid_util.py:164-175) of the
+    current grids, checked by the oracle's cell-by-cell restatement, along a
+    random rollout (owners up to 15: every darkening cycle). N*H*W % 4 != 0 for
+    the 9x7 case exercises the byte-wise tail."""
+    from marlenv import SnakeVecEnv
+    from oracle.snake_oracle import rgb_from_grid
+    N = 37
+    v = SnakeVecEnv(N, num_snakes=S, seed=77, **kw)
+    v.reset()
+    rs = np.random.RandomState(4)
+    for t in range(25):
+        if t % 8 == 0:
+            rgb, grids = _np(v.render_rgb()), _np(v.grids())
+            assert rgb.shape == (N, kw['height'], kw['width'], 3) and rgb.dtype == np.uint8
+            for i in range(N):
+                np.testing.assert_array_equal(rgb[i], rgb_from_grid(grids[i]), err_msg=f'S{S} t{t} env {i}')
+        v.step(torch.from_numpy(rs.randint(0, 3, size=(N, S))))
+
+
+def test_compat_render_modes(tmp_path):
+    """SnakeEnv.render: 'rgb_array' frame, 'gif' frames + save_gif (snake_env.py:267-296, 419-437)."""
+    from marlenv.envs.snake_env import SnakeEnv
+    from oracle.snake_oracle import rgb_from_grid
+    np.random.seed(3)
+    env = SnakeEnv(num_snakes=4)
+    env.reset()
+    for _ in range(3):
+        env.step([0, 1, 2, 0])
+        np.testing.assert_array_equal(env.render('rgb_array'), rgb_from_grid(env.grid))
+        env.render('gif')
+    assert len(env.frame_buffer) == 3 and env.frame_buffer[0].size == (300, 300)
+    fp = env.save_gif(str(tmp_path / 'play.gif'))
+    assert (tmp_path / 'play.gif').stat().st_size > 0 and fp.endswith('play.gif')

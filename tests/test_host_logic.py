@@ -54,3 +54,14 @@ def test_reference_import_paths_resolve():
     assert make_snake is marlenv.make_snake
     assert se.SnakeEnv is marlenv.SnakeEnv
     assert issubclass(RenderGUI, marlenv.wrappers.Wrapper)
+
+
+def test_render_palette_matches_reference():
+    """The palette the product hands snake_render_rgb == the reference's colour
+    of every (code, owner) (tests/golden/render.npz, from grid_util.rgb_from_grid)."""
+    from marlenv.core.render import palette, upscale
+    import golden_io as G
+    z = G.load('render.npz')
+    np.testing.assert_array_equal(palette(), z['palette'])
+    big = upscale(z['rgb'][0])
+    assert big.shape == (300, 300, 3) and (big[::15, ::15] == z['rgb'][0]).all()

@@ -125,3 +125,12 @@ def test_invalid_action_is_keyerror(oracle):
     env.reset()
     with pytest.raises(KeyError):
         env.step([0, 3])
+
+
+def test_rgb_from_grid_golden():
+    """oracle.rgb_from_grid == the reference's rgb_from_grid (grid_util.py:164-175)
+    on the fixture grids, owners 0..15 included (0.7**cycle darkening)."""
+    from oracle.snake_oracle import rgb_from_grid
+    z = G.load('render.npz')
+    for g, want in zip(z['grids'], z['rgb']):
+        np.testing.assert_array_equal(rgb_from_grid(g), want)
