@@ -1248,7 +1248,8 @@ hipEvent_t pooled_event()
         return ev;
     }
     hipEvent_t ev = nullptr;
-    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    // device-scope release: a timing event need not write the L2 back for the host
+    if (hipEventCreateWithFlags(&ev, hipEventReleaseToDevice) != hipSuccess) return nullptr;
     return ev;
 }
 }  // namespace
@@ -1334,6 +1335,13 @@ struct SideCtx {
     hipEvent_t fork, join;
 };
 
+// The fork/join events only order kernels of one device: no system-scope fence
+// (that would write the L2s back for a host that never looks). Stream
+// write/wait-value packets on signal memory were tried for the fork/join and
+// measured no faster in the step (scripts/microbench/forkjoin.hip shows them
+// cheaper in isolation).
+constexpr unsigned kJoinFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+
 static int side_ctx(hipStream_t main, SideCtx *out)
 {
     static std::mutex mu;
@@ -1348,8 +1356,8 @@ static int side_ctx(hipStream_t main, SideCtx *out)
     if (it == ctx.end()) {
         SideCtx c;
         if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c.join, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&c.fork, kJoinFlags) != hipSuccess ||
+            hipEventCreateWithFlags(&c.join, kJoinFlags) != hipSuccess) {
             set_error("side stream / event creation failed");
             return SNAKE_E_LAUNCH;
         }

@@ -13,6 +13,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, 'marl-snake_amd'), ROOT]
@@ -22,14 +23,23 @@ import torch  # noqa: E402
 from marlenv import SnakeVecEnv  # noqa: E402
 
 
-def timed(fn, reps):
+HOST = {}
+
+
+def timed(fn, reps, key=None):
+    """Device ms per call; the host's enqueue ms per call goes to HOST[key] (when
+    it approaches the device time the loop is host-bound)."""
     s = torch.cuda.current_stream()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(s)
+    t0 = time.perf_counter()
     for _ in range(reps):
         fn()
+    t1 = time.perf_counter()
     b.record(s)
     torch.cuda.synchronize()
+    if key is not None:
+        HOST.setdefault(key, []).append((t1 - t0) * 1e3 / reps)
     return a.elapsed_time(b) / reps
 
 
@@ -65,13 +75,14 @@ def main():
     for r in range(a.rounds):
         for p in a.libs:
             v, f = envs[p]
-            res[p]['auto'].append(timed(lambda: v.step(nxt()), a.steps))
+            res[p]['auto'].append(timed(lambda: v.step(nxt()), a.steps, key=p))
             f.reset()
             res[p]['fresh'].append(timed(lambda: f.step(nxt()), 8))
     out = {'N': N, 'cfg': a.cfg}
     for p in a.libs:
         out[os.path.basename(p)] = {k: {'median_ms': round(statistics.median(x), 4), 'min_ms': round(min(x), 4)}
                                     for k, x in res[p].items()}
+        out[os.path.basename(p)]['auto']['host_enqueue_ms'] = round(statistics.median(HOST[p]), 4)
     print(json.dumps(out), flush=True)
 
 

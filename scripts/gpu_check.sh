@@ -29,6 +29,11 @@ for s in "$@"; do
         rlat) step rlat 300 python scripts/perf_probe.py --reset-latency ;;
         stamps) step stamps 300 python scripts/reset_stamps.py marl-snake_amd/build/libsnake_stamps.so ;;
         lat) step lat 120 scripts/microbench/lat ;;
+        gap) step gap 300 scripts/microbench/gap ;;
+        forkjoin) step forkjoin 300 scripts/microbench/forkjoin ;;
+        profserial) export SNAKE_LIB=marl-snake_amd/build/var/libsnake_${PROFLIB:-serial}.so
+                    step profserial 600 rocprofv3 --kernel-trace -d gpurun_out/prof_${PROFLIB:-serial} -o run --output-format csv -- python3 bench.py --steps 100 --warmup 50 --no-cpu-baseline --timing-stride 0
+                    unset SNAKE_LIB ;;
         dbpmc) step dbpmc 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SMEM --kernel-include-regex drawbench --output-format csv -d gpurun_out/dbpmc -o pmc -- python3 scripts/drawbench.py marl-snake_amd/build/db/libsnake_base.so ;;
         drawbench) for f in marl-snake_amd/build/db/*.so; do step drawbench 120 python scripts/drawbench.py $f; done ;;
         obsprof) step obsprof 300 python scripts/obs_profile.py marl-snake_amd/build/libsnake_stamps.so ;;
