@@ -159,7 +159,7 @@ def main():
     torch.cuda.synchronize(device)
 
     L = _native.lib()
-    for k in ('k_logic', 'k_autoreset', 'k_encode', 'resets'):
+    for k in ('k_logic', 'k_autoreset', 'k_encode', 'resets', 'spawn_hits', 'spawn_jobs'):
         _native.timing_read(k, L)                      # drop anything from the warmup
     stride = args.timing_stride
     if distributed:
@@ -183,6 +183,10 @@ def main():
         ms, n = _native.timing_read(k, L)
         kern[k] = ms / max(n, 1)
     resets = _native.timing_read('resets', L)[1]
+    # spawn-ahead counters (counted on the timed-event steps only)
+    n_timed = len(range(0, args.steps, stride)) if stride > 0 else 0
+    sp_hits = _native.timing_read('spawn_hits', L)[1]
+    sp_jobs = _native.timing_read('spawn_jobs', L)[1]
 
     red = reduce_max([elapsed] + list(kern.values()), device, dist if distributed else None)
     elapsed, kern = red[0], dict(zip(kern, red[1:]))
@@ -236,6 +240,10 @@ def main():
                           'frac': round(step_gbs / HBM_PEAK_GBS, 4), 'bytes_per_env_step': B},
         'kernels': {k: round(v, 4) for k, v in kern.items()},
         'resets_per_step': round(resets / args.steps, 1),
+        'spawn_ahead': ({'hits_per_step': round(sp_hits / n_timed, 1),
+                         'jobs_per_step': round(sp_jobs / n_timed, 1),
+                         'hit_rate': round(sp_hits / n_timed / max(resets / args.steps, 1e-9), 4)}
+                        if n_timed else None),
         'cpu_baseline': None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 6
+#define SNAKE_ABI_VERSION 7
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -50,6 +50,10 @@ typedef struct {
     int32_t autoreset;          /* 1 = reset an env inside snake_step when all its dones
                                    are True and return the reset obs (vector-env semantics,
                                    wrappers.py:139-145); 0 = return the terminal obs */
+    int32_t spawn_ahead;        /* spawn-ahead threshold (snake_step): 0 = default (at most
+                                   2 live snakes, every env under coop; the environment
+                                   variable SNAKE_SPAWN_THR overrides), -1 = off, k >= 1 =
+                                   envs with at most k live snakes. Never changes results. */
 } snake_cfg;
 
 /* Byte sizes of every caller-allocated buffer for num_envs envs (snake_plan). */
@@ -57,13 +61,17 @@ typedef struct {
     int64_t grid;       /* uint8  [N][fs][grid_stride]   grid ring (newest = env[2]) */
     int64_t snake;      /* int32  [N][S][4]              packed snake records */
     int64_t body;       /* uint8  [N][S][ring_cap]       direction deques (rings) */
-    int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos */
+    int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos,
+                                                         spawn-ahead status (0 none, 1 partial, 2 ready) */
     int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */
     int64_t stats;      /* double [N][4][S]              episode scores/steps/fruits/kills */
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
     int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
     int64_t jscratch;   /* uint32 [min(N,2048)][round4(n_cand)+64] reset link tables, 0 if in LDS */
-    int64_t resetq;     /* int32  [64][cap] + [2][64]    sharded auto-reset queue + counters */
+    int64_t spawn;      /* uint32 [N][656]               spawn-ahead record: MT key, MT pos and the
+                                                         S spawn-pose indices of the env's next reset */
+    int64_t resetq;     /* int32  [2][64][cap] + [2][160] sharded auto-reset and spawn-ahead queues
+                                                         + per-step counters */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */
     int64_t rew;        /* double [N][S] */
     int64_t done;       /* uint8  [N][S] */
@@ -86,6 +94,7 @@ typedef struct {        /* device state buffers (layouts in snake_layout) */
     uint32_t *mt;
     const int16_t *cand;
     uint32_t *jscratch; /* may be NULL when layout.jscratch == 0 */
+    uint32_t *spawn;
     int32_t  *resetq;   /* zero-initialised once by the caller */
 } snake_state;
 
@@ -123,7 +132,20 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
  * the same call and its out->obs holds the reset observation. Launches: k_logic
  * (the game rules of every env, queueing the auto-resets), then k_autoreset on
  * `stream` concurrently with k_encode (every other env's observation) on a side
- * stream the library keeps per caller stream; joined before the call returns. */
+ * stream the library keeps per caller stream; joined before the call returns.
+ *
+ * Spawn-ahead: a reset's spawn poses depend only on the env's MT19937 state, which
+ * changes only at fruit respawns and resets. With autoreset, k_logic also queues
+ * every env that is close to the end of its episode (at most 2 snakes alive, or
+ * any env under coop) and has no ready record for its current MT state, and the
+ * k_autoreset workers, after the step's resets, run one permutation attempt of
+ * that env's NEXT reset into its spawn record (st->spawn). A later reset of the
+ * env starts from the record (MT key, position, poses) when no draw has touched
+ * the MT state since; a fruit respawn or a reset invalidates it. Results are
+ * identical with or without it (it only moves draws off the step's critical
+ * path); cfg->spawn_ahead = -1 disables it. A caller that
+ * rewrites an env's MT key or position itself must zero that env's status word
+ * (env word 4). */
 int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
                const int8_t *actions, const snake_out *out, void *stream);
 
@@ -141,7 +163,9 @@ int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_en
  * is bracketed by timing events on its own stream. snake_timing_read returns the
  * summed device time (ms) and the launch count of one kernel ("k_logic",
  * "k_autoreset", "k_encode", "k_reset") since its last read, and the number of
- * auto-resets run (kernel "resets": count only); it waits for the events. */
+ * auto-resets run (kernel "resets": count only); it waits for the events.
+ * "spawn_hits" / "spawn_jobs" count (while enabled) the auto-resets that started
+ * from a ready spawn-ahead record and the spawn-ahead attempts run. */
 int snake_timing_enable(int on);
 int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
 

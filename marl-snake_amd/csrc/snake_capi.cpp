@@ -3,6 +3,7 @@
 // HIP launches in snake_kernels.hip.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -201,12 +202,13 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     // when small, else one global table per reset worker.
     const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
     o->jscratch = (link <= kLinkLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
-    {   // auto-reset queue: kQShards shards (k_logic block % kQShards), each with room
-        // for every env of its blocks, + two parities of per-shard counters
+    o->spawn = N * kSpawnStride * 4;
+    {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
+        // kQShards) with room for every env of its blocks, + two parities of counters
         const int64_t E = kWave / (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
         const int64_t blocks = (N + E - 1) / E;
         const int64_t cap = (blocks + kQShards - 1) / kQShards * E;
-        o->resetq = (kQShards * cap + 2 * kQShards) * 4;
+        o->resetq = (2 * kQShards * cap + 2 * kQCounters) * 4;
     }
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
@@ -277,12 +279,24 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     }
     k->link_stride = (int)round_up(k->n_cand, 4) + kWave;
     k->link_in_lds = 4 * k->link_stride <= kLinkLdsMax;
-    k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
+    // tuning knobs (A/B probes): workers of k_autoreset (<= kResetSlots, the
+    // global link tables are sized for that) and the spawn-ahead wave priority
+    static const char *ev_slots = getenv("SNAKE_RESET_SLOTS");
+    static const char *ev_prio = getenv("SNAKE_SPAWN_PRIO");
+    const int slots = ev_slots ? std::max(1, std::min(kResetSlots, atoi(ev_slots))) : kResetSlots;
+    k->reset_slots = (int)std::min<int64_t>(N, slots);
+    k->spawn_prio = ev_prio ? std::max(0, std::min(3, atoi(ev_prio))) : 1;
     k->q_envs_per_block = kWave / (k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16));
     {
         const int64_t blocks = (N + k->q_envs_per_block - 1) / k->q_envs_per_block;
         k->q_cap = (int)((blocks + kQShards - 1) / kQShards * k->q_envs_per_block);
     }
+    // spawn-ahead: by default envs with at most 2 live snakes (any env
+    // under coop, where one death ends the episode); -1 = off
+    static const char *ev = getenv("SNAKE_SPAWN_THR");
+    if (c->spawn_ahead != 0) k->spawn_thr = c->spawn_ahead < 0 ? -1 : c->spawn_ahead;
+    else k->spawn_thr = ev ? atoi(ev) : (k->coop ? k->S : 2);
+    if (!k->autoreset) k->spawn_thr = -1;
     k->lds_obs_bytes = off;
     k->lds_link = off;
     if (k->link_in_lds) off += 4 * k->link_stride;
@@ -303,8 +317,8 @@ static int check_state(const KCfg &k, const snake_state *st, bool need_all)
         set_error("snake_state has a NULL buffer");
         return SNAKE_E_ARG;
     }
-    if (!st->resetq) {
-        set_error("snake_state.resetq is NULL");
+    if (!st->resetq || !st->spawn) {
+        set_error("snake_state.resetq / spawn is NULL");
         return SNAKE_E_ARG;
     }
     if (!k.link_in_lds && !st->jscratch) {

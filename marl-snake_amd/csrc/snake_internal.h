@@ -16,9 +16,15 @@ constexpr int kLinkLdsMax = 16384;  // bytes of a reset link table kept in LDS
 constexpr int kResetSlots = 2048;   // concurrent reset workers (global link tables)
 constexpr int kQShards = 64;        // auto-reset queue shards (k_logic block % 64)
 constexpr int kStageMax = 8192;     // bytes of staged observation per encode group
+constexpr int kSpawnStride = 656;   // u32 words per spawn-ahead record: key, pos, poses
+constexpr int kSpawnPos = 624;      // record word: MT position after the recorded attempts
+constexpr int kSpawnSel = 625;      // record words [625, 625 + S): spawn-pose indices
+constexpr int kQCounters = 160;     // per-parity queue counters: 64 reset, 64 spawn, claim
 
 // env record words
-enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3 };
+enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4 };
+// spawn-ahead status (env word ENV_SPAWN)
+enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2 };
 
 // Everything a kernel needs, by value (a kernel argument).
 struct KCfg {
@@ -43,6 +49,9 @@ struct KCfg {
     int reset_slots;            // min(N, kResetSlots)
     int q_envs_per_block;       // envs per k_logic block (64 / MS)
     int q_cap;                  // queue entries per shard
+    int spawn_thr;              // queue spawn-ahead when <= this many snakes live (-1: off)
+    int spawn_prio;             // wave priority of the spawn-ahead jobs (resets: 3)
+    int diag;                   // count spawn-ahead hits/jobs (while timing is enabled)
     double rf, rk, rl, rw, rt, max_steps;
 };
 

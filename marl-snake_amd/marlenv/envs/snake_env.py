@@ -83,9 +83,7 @@ class SnakeEnv:
         torch = _torch()
         st = np.random.get_state(legacy=True)
         key = np.ascontiguousarray(np.asarray(st[1], dtype=np.uint32)).view(np.int32)
-        mt, pos = self._vec.mt_state()
-        mt[0].copy_(torch.from_numpy(key), non_blocking=False)
-        pos[0] = int(st[2])
+        self._vec.set_mt_state(0, torch.from_numpy(key), int(st[2]))
 
     def _pull_rng(self):
         if self._rng != 'global':

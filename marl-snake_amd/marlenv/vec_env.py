@@ -66,6 +66,7 @@ class SnakeVecEnv:
         self.stats = buf(lay.stats, torch.float64)
         self.mt = buf(lay.mt, torch.int32)
         self.jscratch = buf(lay.jscratch, torch.int32) if lay.jscratch else None
+        self.spawn = buf(lay.spawn, torch.int32)
         self.resetq = buf(lay.resetq, torch.int32)
         cap = int(lay.n_cand) * self.cfg.snake_length
         host = np.zeros(cap, np.int16)
@@ -76,7 +77,7 @@ class SnakeVecEnv:
             self.grid.data_ptr(), self.snake.data_ptr(), self.body.data_ptr(), self.env_rec.data_ptr(),
             self.ctr.data_ptr(), self.stats.data_ptr(), self.mt.data_ptr(), self.cand.data_ptr(),
             self.jscratch.data_ptr() if self.jscratch is not None else None,
-            self.resetq.data_ptr())
+            self.spawn.data_ptr(), self.resetq.data_ptr())
         check(L.snake_seed(ctypes.byref(self.cfg), ctypes.byref(self._state), N, self.seed_base,
                            self.env_offset, self._stream()))
 
@@ -203,8 +204,18 @@ class SnakeVecEnv:
                             y & 3, (y >> 8) & 1, ((z >> 16) & 0xffff) + 1], dim=-1)
 
     def mt_state(self):
-        """(N, 624) MT19937 keys (int32 view of uint32) and (N,) positions."""
+        """(N, 624) MT19937 keys (int32 view of uint32) and (N,) positions (read-only
+        use: writers go through set_mt_state)."""
         return self.mt.view(self.num_envs, 624), self.env_rec.view(self.num_envs, 8)[:, 3]
+
+    def set_mt_state(self, i, key, pos):
+        """Overwrite env i's MT19937 key (624 uint32, as int32) and position; voids
+        its spawn-ahead record (include/snake_env.h), which was drawn from the old state."""
+        torch = _torch()
+        er = self.env_rec.view(self.num_envs, 8)
+        self.mt.view(self.num_envs, 624)[i].copy_(torch.as_tensor(key).to(self.device))
+        er[i, 3] = int(pos)
+        er[i, 4] = 0
 
     def inject(self, i, grid, snakes, alive_snakes, episode_length=0):
         """Overwrite env i with a crafted state (the env.grid / env.snakes assignment

@@ -23,6 +23,22 @@ for s in "$@"; do
         testsv) step tests 300 python -m pytest tests -q -m gpu -rf ;;
         bench) step bench 600 python bench.py ;;
         benchq) step bench 300 python bench.py --steps 200 --warmup 50 --cpu-seconds 5 ;;
+        benchthr) for t in ${THRS:--1 1 2 3}; do
+                      export SNAKE_SPAWN_THR=$t
+                      step benchthr$t 300 python bench.py --no-cpu-baseline --steps 1000
+                  done
+                  unset SNAKE_SPAWN_THR ;;
+        benchab) # VARS="A=1 B=2;A=3" : one short bench per ';'-separated env setting
+                 IFS=';' read -ra sets <<< "$VARS"
+                 i=0
+                 for kv in "${sets[@]}"; do
+                     i=$((i+1))
+                     echo "-- set $i: $kv"
+                     env $kv timeout -k 10 300 python bench.py --no-cpu-baseline --steps 1000 > gpurun_out/benchab$i.log 2>&1
+                     rc=$?
+                     echo "benchab$i rc=$rc"; tail -1 gpurun_out/benchab$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['kernels'], d.get('spawn_ahead'))"
+                     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fault-like exit $rc: stopping"; exit $rc; fi
+                 done ;;
         benchnt) step benchnt 300 python bench.py --timing-stride 0 --no-cpu-baseline ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 300 --warmup 100 --no-cpu-baseline ;;
         probe) step probe 600 python scripts/perf_probe.py ;;

@@ -132,6 +132,11 @@ BATCH_CASES = {
     'single_s1': (dict(height=10, width=10, vision_range=4, num_fruits=4), 1, 64, 300),
     'trunc_s2': (dict(height=12, width=12, max_episode_steps=7), 2, 64, 100),
     's16': (dict(height=24, width=24, snake_length=2, vision_range=3), 16, 16, 200),
+    # spawn-ahead for every env (include/snake_env.h): nearly every reset starts
+    # from a ready record, partial records carry retries across steps
+    'spawn_all_vr5': (dict(height=20, width=20, snake_length=3, vision_range=5, spawn_ahead=4), 4, 96, 300),
+    'spawn_off_vr5': (dict(height=20, width=20, snake_length=3, vision_range=5, spawn_ahead=-1), 4, 32, 150),
+    'spawn_all_40_s8': (dict(height=40, width=40, snake_length=3, vision_range=5, spawn_ahead=8), 8, 16, 250),
 }
 
 
@@ -142,7 +147,8 @@ def test_batch_matches_oracle(oracle, case):
     seed = 1000 + 17 * len(case)
     v = SnakeVecEnv(N, num_snakes=S, seed=seed, **kw)
     obs0 = _np(v.reset())
-    refs, robs = oracle_batch(oracle, N, seed, S, **kw)
+    okw = {k: v for k, v in kw.items() if k != 'spawn_ahead'}   # a GPU scheduling knob only
+    refs, robs = oracle_batch(oracle, N, seed, S, **okw)
     np.testing.assert_array_equal(obs0, robs)
     rs = np.random.RandomState(seed)
     n_act = 5 if kw.get('observer') == 'human' else 3
@@ -229,6 +235,63 @@ def test_full_size_sampled_parity(oracle):
         assert int(heads[~alive].sum()) == 0
         assert not bool(info['error'].any())
     assert n_ep > 0.005 * N * T / 60
+
+
+@pytest.mark.parametrize('S,kw,spawn', [
+    (4, dict(height=20, width=20, vision_range=5), (0, -1, 1, 4)),
+    (4, dict(height=12, width=12, coop=True), (0, -1)),             # coop: every env queued
+    (8, dict(height=40, width=40, vision_range=5, frame_stack=2), (0, -1)),   # global link tables
+])
+def test_spawn_ahead_is_invisible(S, kw, spawn):
+    """The spawn-ahead records only move reset draws off the critical path: every
+    threshold gives bit-identical rollouts, and the default one actually serves
+    resets from ready records."""
+    from marlenv import SnakeVecEnv, _native
+    N, T = 1024, 160
+    envs = [SnakeVecEnv(N, num_snakes=S, seed=77, spawn_ahead=sp, **kw) for sp in spawn]
+    outs = [v.reset() for v in envs]
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    g = torch.Generator(device='cuda').manual_seed(4)
+    for k in ('resets', 'spawn_hits', 'spawn_jobs'):
+        _native.timing_read(k)
+    hits = jobs = 0
+    for t in range(T):
+        a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        res = []
+        for j, v in enumerate(envs):
+            if j == 0:
+                _native.timing_enable(True)
+            res.append(v.step(a))
+            if j == 0:
+                _native.timing_enable(False)
+                hits += _native.timing_read('spawn_hits')[1]
+                jobs += _native.timing_read('spawn_jobs')[1]
+        o0, r0, d0, i0 = res[0]
+        for o, r, d, i in res[1:]:
+            assert torch.equal(o0, o) and torch.equal(r0, r) and torch.equal(d0, d), f'step {t}'
+            assert torch.equal(i0['episode_done'], i['episode_done'])
+        for v in envs[1:]:
+            assert torch.equal(envs[0].grids(), v.grids())
+    assert jobs > 0 and hits > 0
+
+
+def test_set_mt_state_voids_spawn_records():
+    """Rewriting an env's MT state (compat env's global-RNG sync) must void its
+    spawn-ahead record: the next reset draws from the new state."""
+    from marlenv import SnakeVecEnv
+    N, S = 64, 4
+    kw = dict(height=10, width=10, num_snakes=S, seed=3, spawn_ahead=4)
+    a, b = SnakeVecEnv(N, **kw), SnakeVecEnv(N, **dict(kw, spawn_ahead=-1))
+    a.reset(), b.reset()
+    g = torch.Generator(device='cuda').manual_seed(0)
+    for t in range(30):   # builds ready records in `a`
+        act = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        a.step(act), b.step(act)
+    key = torch.from_numpy(np.random.RandomState(11).randint(0, 2 ** 31, 624).astype(np.int32))
+    for v in (a, b):
+        for i in range(N):
+            v.set_mt_state(i, key, 624)
+    assert torch.equal(a.reset(), b.reset())
 
 
 def test_invalid_actions():
