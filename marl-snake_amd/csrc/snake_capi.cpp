@@ -198,10 +198,11 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->stats = N * 4 * S * 8;
     o->mt = N * kMtN * 4;
     o->cand = o->n_cand * c->snake_length * 2;
-    // Link tables of the resets in flight (snake_kernels.hip perm_trace): in LDS
-    // when small, else one global table per reset worker.
+    // What the reset workers record of a permutation (snake_kernels.hip
+    // perm_trace): the u16 draw record in LDS up to kJarrLdsMax bytes, else one
+    // global u32 link table per reset worker.
     const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
-    o->jscratch = (link <= kLinkLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
+    o->jscratch = (round_up(2 * o->n_cand, 16) <= kJarrLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     o->spawn = N * kSpawnStride * 4;
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
         // kQShards) with room for every env of its blocks, + two parities of counters
@@ -276,9 +277,12 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         k->mag_fsoh = (uint32_t)(((1ull << 32) + fsoh - 1) / fsoh);
         k->mag_oh = (uint32_t)(((1ull << 32) + oh - 1) / oh);
         k->mag_W = (uint32_t)(((1ull << 32) + k->W - 1) / k->W);
+        const uint64_t n16 = (uint64_t)k->grid_stride / 16;
+        k->mag_n16 = (uint32_t)(((1ull << 32) + n16 - 1) / n16);
     }
     k->link_stride = (int)round_up(k->n_cand, 4) + kWave;
-    k->link_in_lds = 4 * k->link_stride <= kLinkLdsMax;
+    const int jbytes = (int)round_up(2 * (int64_t)k->n_cand, 16);   // the LDS draw record
+    k->link_in_lds = jbytes <= kJarrLdsMax;
     // tuning knobs (A/B probes): workers of k_autoreset (<= kResetSlots, the
     // global link tables are sized for that) and the spawn-ahead wave priority
     static const char *ev_slots = getenv("SNAKE_RESET_SLOTS");
@@ -298,9 +302,10 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     else k->spawn_thr = ev ? atoi(ev) : (k->coop ? k->S : 2);
     if (!k->autoreset) k->spawn_thr = -1;
     k->lds_obs_bytes = off;
-    k->lds_link = off;
-    if (k->link_in_lds) off += 4 * k->link_stride;
-    k->lds_bytes = off;
+    // the reset workers never use the encode staging buffer: the draw record
+    // overlays it (the workers' LDS is what k_encode's waves share the CUs with)
+    k->lds_link = k->lds_stage;
+    k->lds_bytes = k->link_in_lds ? std::max(off, k->lds_stage + jbytes) : off;
     if (k->lds_bytes > 64 * 1024) {
         set_error("grid ring of %d bytes per env does not fit the LDS budget", k->ring_bytes);
         return SNAKE_E_CONFIG;

@@ -12,7 +12,7 @@ constexpr int kMtN = 624;
 constexpr int kMaxSnakes = 16;
 constexpr int kMaxFruits = 64;
 constexpr int kEnvRec = 8;          // int32 words per env record
-constexpr int kLinkLdsMax = 16384;  // bytes of a reset link table kept in LDS
+constexpr int kJarrLdsMax = 36864;  // bytes of a reset's u16 draw record kept in LDS
 constexpr int kResetSlots = 2048;   // concurrent reset workers (global link tables)
 constexpr int kQShards = 64;        // auto-reset queue shards (k_logic block % 64)
 constexpr int kStageMax = 8192;     // bytes of staged observation per encode group
@@ -38,7 +38,10 @@ struct KCfg {
     int adv_f, adv_j, adv_i, adv_k;
     // dynamic LDS carve (bytes, 16-aligned)
     int lds_frames, lds_centers, lds_fruit, lds_link, lds_bytes, link_in_lds;
-    int link_stride;            // round4(n_cand) + 64 per-lane dummies: u32 entries of a link table
+    // link_in_lds: the draws record j_i (u16 per i) in LDS at lds_link; else each
+    // worker's u32 link table in global scratch, link_stride = round4(n_cand) + 64
+    // per-lane dummies entries per table
+    int link_stride;
     int lds_obs_bytes;          // LDS of k_encode: no reset worker state
     // row-wise encode through an LDS staging buffer (encode_rows): snakes per
     // staged group (0: direct encode), the buffer, and magic reciprocals of
@@ -46,6 +49,7 @@ struct KCfg {
     int enc_group, lds_stage;
     uint32_t mag_fsoh, mag_oh;
     uint32_t mag_W;             // x / W == umulhi(x, mag_W) for cell indices x < H*W
+    uint32_t mag_n16;           // q / (grid_stride/16) == umulhi(q, mag_n16) for q < 2^32/n16
     int reset_slots;            // min(N, kResetSlots)
     int q_envs_per_block;       // envs per k_logic block (64 / MS)
     int q_cap;                  // queue entries per shard

@@ -366,7 +366,11 @@ __device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base,
         A = k;
     }
     const int ii0 = i - mbcnt64(a0), ii1 = (i - A0) - mbcnt64(a1);
-    if (__builtin_expect(i - A + 1 < S, 0)) {   // the last rounds: some indices < S
+    if constexpr (std::is_same<NP, lu16>::value) {
+        // LDS draw record: j_i at index i, exactly one writer per index
+        if (inv_ballot(a0)) link[ii0] = (uint16_t)w0;
+        if (inv_ballot(a1)) link[ii1] = (uint16_t)w1;
+    } else if (__builtin_expect(i - A + 1 < S, 0)) {   // the last rounds: some indices < S
         if (inv_ballot(a0)) perm_record(ii0, w0, S, link, jsmall);
         if (inv_ballot(a1)) perm_record(ii1, w1, S, link, jsmall);
     } else {
@@ -416,6 +420,50 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
         }
     }
     COUNT_FLUSH(e, lane);
+}
+
+// Final arr[k] of the Fisher-Yates pass for k < S from the LDS draw record
+// (jarr[i] = j_i): replay the swaps i < S on lane k's position k, then scan
+// i = S .. n-1 in order, 256 at a time: a tracked position x moves to i exactly
+// when j_i == x (the swap brings arr[i] there; x < i always). Every tracked
+// position is tested against a chunk with one ballot; a hit re-tests the rest
+// of the chunk from the new position.
+template <int MS>
+__device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int lane)
+{
+    int x = lane;
+    for (int i = 1; i < S; i++) {
+        const int j = jarr[i];
+        x = (x == i) ? j : (x == j ? i : x);
+    }
+    int xk[MS];
+#pragma unroll
+    for (int k = 0; k < MS; k++) xk[k] = bcast(x, k);
+    for (int base = S; base < n; base += 4 * kWave) {
+        int jv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = base + u * kWave + lane;
+            jv[u] = (int)jarr[min(i, n - 1)];
+            jv[u] = i < n ? jv[u] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+#pragma unroll
+            for (int k = 0; k < MS; k++) {
+                if (k < S) {
+                    unsigned long long m = __ballot(jv[u] == xk[k]);
+                    while (m) {
+                        const int l = __ffsll((long long)m) - 1;
+                        xk[k] = base + u * kWave + l;
+                        m = __ballot(jv[u] == xk[k]);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < MS; k++) q[k] = xk[k];
 }
 
 // Final arr[k] of the Fisher-Yates pass for k < S, lane k: walk position k
@@ -621,20 +669,28 @@ template <int MS, bool JL>
 __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, uint8_t *lds, int slot,
                               int e, int attempt, int (&q)[MS], int &cell, int lane)
 {
-    // the permutation's link table: LDS when it fits the budget, else global scratch
-    typedef typename std::conditional<JL, lu32, gu32>::type NP;
-    NP *link = JL ? (NP *)(lds + c.lds_link) : (NP *)(st.jscratch + (int64_t)slot * c.link_stride);
-    lu16 *jsmall = (lu16 *)(lds + c.lds_fruit);   // the fruit buffer is free until place_fruits
     const int S = c.S, L = c.L, SL = S * L;
     const int sk = lane / L, si = lane - sk * L;
     STAMP(e, lane, 1 + 3 * min(attempt, 3));
-    for (int x = 4 * lane; x < c.link_stride - kWave; x += 4 * kWave)
-        *(typename std::conditional<JL, lu4, gu4>::type *)(link + x) = (v4u32)kNoLink;
-    if (JL) wave_sync(); else __syncthreads();
-    mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, lane, e);
-    STAMP(e, lane, 2 + 3 * min(attempt, 3));
-    if (JL) wave_sync(); else __syncthreads();   // the link table, written by every lane
-    perm_trace<MS>(S, link, jsmall, q, lane);
+    if constexpr (JL) {
+        // the u16 draw record in LDS: every index 1..n-1 is written, nothing to clear
+        lu16 *jarr = (lu16 *)(lds + c.lds_link);
+        mt_perm_draws(mt, c.n_cand, S, jarr, c.n_cand, jarr, lane, e);
+        STAMP(e, lane, 2 + 3 * min(attempt, 3));
+        wave_sync();
+        perm_trace_j<MS>(S, c.n_cand, jarr, q, lane);
+    } else {
+        // large boards: the link table in this worker's global scratch
+        gu32 *link = (gu32 *)(st.jscratch + (int64_t)slot * c.link_stride);
+        lu16 *jsmall = (lu16 *)(lds + c.lds_fruit);   // the fruit buffer is free until place_fruits
+        for (int x = 4 * lane; x < c.link_stride - kWave; x += 4 * kWave)
+            *(gu4 *)(link + x) = (v4u32)kNoLink;
+        __syncthreads();
+        mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, lane, e);
+        STAMP(e, lane, 2 + 3 * min(attempt, 3));
+        __syncthreads();   // the link table, written by every lane
+        perm_trace<MS>(S, link, jsmall, q, lane);
+    }
     STAMP(e, lane, 3 + 3 * min(attempt, 3));
     int pk = 0;
 #pragma unroll
@@ -806,8 +862,12 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // ---- every load this step needs, issued up front
     int4 er = make_int4(0, 0, 0, 0);
     int spst = SPAWN_NONE;
-    if (env_ok) er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
-    if (env_ok && c.spawn_thr >= 0) spst = st.env[(int64_t)e * kEnvRec + ENV_SPAWN];
+    if (env_ok) {
+        er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
+        // loaded whatever the threshold: a step run with spawn-ahead off must
+        // still void a record its fruit draws make stale
+        spst = st.env[(int64_t)e * kEnvRec + ENV_SPAWN];
+    }
     int4 rec = make_int4(0, 0, 0, 0);
     int act = 0;
     double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
@@ -818,17 +878,34 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         s0 = sp[k]; s1 = sp[S + k]; s2 = sp[2 * S + k]; s3 = sp[3 * S + k];
     }
     const int alive0 = er.x, eplen = er.y, cur = er.z, mtpos = er.w;
-    {   // stage the E current frames: env g's at lds + g * stride
+    // stage the E current frames (env g's at lds + g * stride): eight 16-B loads
+    // in flight per lane before the LDS writes (a load-wait-write loop pays one
+    // memory round trip per 64 chunks). Branch-free: tail lanes re-stage the last
+    // chunk, the missing envs of a partial block stage the last env. With one
+    // frame the slot is 0 and the loads do not wait for the env records.
+    auto stage = [&](auto one) {
+        constexpr bool ONE = decltype(one)::value;
         const uint4 *src = reinterpret_cast<const uint4 *>(st.grid);
         uint4 *d4 = reinterpret_cast<uint4 *>(lds);
-        // uniform trip count: __shfl must not read from lanes a divergent loop parked
-        for (int q0 = 0; q0 < E * n16; q0 += kWave) {
-            const int q = q0 + lane, gg = min(q / n16, E - 1), off = q - gg * n16;
-            const int cg = __shfl(cur, gg * G);
-            if (q < E * n16 && e0 + gg < c.N)
-                d4[q] = src[((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)cg * stride) / 16 + off];
+        const int nq = E * n16;
+        for (int q0 = 0; q0 < nq; q0 += 8 * kWave) {   // uniform trip count (the __shfl)
+            uint4 v[8];
+            int qq[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int q = min(q0 + u * kWave + lane, nq - 1);
+                const int gg = (int)__umulhi((uint32_t)q, c.mag_n16), off = q - gg * n16;
+                const int cg = ONE ? 0 : __shfl(cur, gg * G);
+                const int64_t ee = min(e0 + gg, c.N - 1);
+                v[u] = src[(ee * c.ring_bytes + (int64_t)cg * stride) / 16 + off];
+                qq[u] = q;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) d4[qq[u]] = v[u];
         }
-    }
+    };
+    if (fs == 1) stage(std::true_type{});
+    else stage(std::false_type{});
     // keep the statistics loads up here with the others (the compiler would sink
     // them to their first use, deep in the step, and pay a full memory latency there)
     __asm__ volatile("" ::"v"(s0), "v"(s1), "v"(s2), "v"(s3));
@@ -1016,8 +1093,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         uint32_t accm = 0;
 #pragma unroll
         for (int t = 0; t < kRespawnT; t++) {
-            const int pos = mtpos + t * G + k;
-            const uint32_t raw = (draws && room) ? st.mt[(int64_t)e * kMtN + pos] : 0u;
+            const uint32_t raw = (draws && room) ? st.mt[(int64_t)e * kMtN + mtpos + t * G + k] : 0u;
             const uint32_t tv = temper(raw) & rmask;
             rawbuf[t * G + k] = tv;
             accm |= gbits(__ballot(draws && room && tv <= rng)) << (t * G);
@@ -1131,7 +1207,8 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         uint4 *dst = reinterpret_cast<uint4 *>(st.grid);
         const uint4 *s4 = reinterpret_cast<const uint4 *>(lds);
         for (int q0 = 0; q0 < E * n16; q0 += kWave) {
-            const int q = q0 + lane, gg = min(q / n16, E - 1), off = q - gg * n16;
+            const int q = q0 + lane, gg = min((int)__umulhi((uint32_t)q, c.mag_n16), E - 1);
+            const int off = q - gg * n16;
             const int ng = __shfl(ncur, gg * G);
             const int bg = __shfl((int)bad, gg * G);
             if (q < E * n16 && e0 + gg < c.N && !bg)
@@ -1599,14 +1676,12 @@ __global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsi
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
-    snake::lu32 *link = (snake::lu32 *)lds;
-    snake::lu16 *jsmall = (snake::lu16 *)(lds + 4 * (n + 64 + 4));
-    for (int x = lane; x < n + 64; x += 64) link[x] = 0xffffffffu;
+    snake::lu16 *jarr = (snake::lu16 *)lds;   // the LDS draw record of the reset path
     snake::WaveMT mt;
     snake::mt_load(mt, mt_src, pos0, lane);
     snake::wave_sync();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    snake::mt_perm_draws(mt, n, S, link, n, jsmall, lane);
+    snake::mt_perm_draws(mt, n, S, jarr, n, jarr, lane);
     snake::wave_sync();
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) { out[0] = t1 - t0; out[1] = (unsigned long long)mt.pos; }
@@ -1614,7 +1689,7 @@ __global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsi
 
 extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, int S, unsigned long long *out_dev)
 {
-    hipLaunchKernelGGL(k_drawbench, dim3(1), dim3(64), 4 * (n + 64 + 4) + 64, 0, mt_dev, pos0, n, S, out_dev);
+    hipLaunchKernelGGL(k_drawbench, dim3(1), dim3(64), 2 * n + 64, 0, mt_dev, pos0, n, S, out_dev);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 

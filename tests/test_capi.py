@@ -56,7 +56,11 @@ def test_plan_sizes(native):
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
     assert lay.obs_c == 32 and lay.obs == 8192 * 8 * 11 * 11 * 32
-    assert lay.n_cand == 16424 and lay.jscratch == 2048 * (16424 + 64) * 4
+    assert lay.n_cand == 16424 and lay.jscratch == 0              # u16 draw record fits LDS
+    c = cfg(native, height=44, width=44, num_snakes=4)
+    lay2 = native.SnakeLayout()
+    assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay2)) == 0
+    assert lay2.n_cand == 20168 and lay2.jscratch == 2048 * (20168 + 64) * 4   # global link tables
     assert lay.grid == 8192 * 4 * 1600
 
 

@@ -137,6 +137,8 @@ BATCH_CASES = {
     'spawn_all_vr5': (dict(height=20, width=20, snake_length=3, vision_range=5, spawn_ahead=4), 4, 96, 300),
     'spawn_off_vr5': (dict(height=20, width=20, snake_length=3, vision_range=5, spawn_ahead=-1), 4, 32, 150),
     'spawn_all_40_s8': (dict(height=40, width=40, snake_length=3, vision_range=5, spawn_ahead=8), 8, 16, 250),
+    # 20 168 spawn poses: the reset workers' global link tables (no LDS draw record)
+    'big_44_s4_global_links': (dict(height=44, width=44, snake_length=3, vision_range=4, spawn_ahead=4), 4, 16, 200),
 }
 
 
@@ -147,7 +149,7 @@ def test_batch_matches_oracle(oracle, case):
     seed = 1000 + 17 * len(case)
     v = SnakeVecEnv(N, num_snakes=S, seed=seed, **kw)
     obs0 = _np(v.reset())
-    okw = {k: v for k, v in kw.items() if k != 'spawn_ahead'}   # a GPU scheduling knob only
+    okw = {k: x for k, x in kw.items() if k != 'spawn_ahead'}   # a GPU scheduling knob only
     refs, robs = oracle_batch(oracle, N, seed, S, **okw)
     np.testing.assert_array_equal(obs0, robs)
     rs = np.random.RandomState(seed)
