@@ -45,7 +45,7 @@ __device__ unsigned long long g_spawn_jobs;   // spawn-ahead attempts run
 // Diagnostic build only: s_memtime stamps of env 0's wave at phase boundaries.
 __device__ unsigned long long g_stamps[64];
 __device__ unsigned long long g_counts[8];
-__device__ unsigned long long g_obsprof[512];   // realtime (100 MHz) of auto-resets / encodes
+__device__ unsigned long long g_obsprof[768];   // realtime (100 MHz) of auto-resets / encodes / spawn jobs
 #define OBSPROF(slot, lane)                                                          \
     do { if ((lane) == 0) g_obsprof[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define STAMP(e, lane, idx)                                                        \
@@ -1307,8 +1307,10 @@ __global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_stat
             const int sh = __ffsll((long long)__ballot(j >= pexcl && j < pincl)) - 1;
             const int e = st.resetq[(kQShards + sh) * c.q_cap + j - bcast(pexcl, sh)];
             if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
+            if (j < 128) OBSPROF(512 + j, lane);
             if (c.link_in_lds) do_spawn<MS, true>(c, st, e, lds, blockIdx.x, lane);
             else do_spawn<MS, false>(c, st, e, lds, blockIdx.x, lane);
+            if (j < 128) OBSPROF(640 + j, lane);
         }
         int nx = 0;
         if (lane == 0) nx = atomicAdd(&qc[2 * kQShards], 1);
@@ -1696,11 +1698,11 @@ extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, in
 #endif
 
 #ifdef SNAKE_STAMPS
-extern "C" int snake_debug_obsprof(unsigned long long *out /* 512 */)
+extern "C" int snake_debug_obsprof(unsigned long long *out /* 768 */)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_obsprof), sizeof(unsigned long long) * 512) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_obsprof), sizeof(unsigned long long) * 768) != hipSuccess)
         return -1;
-    unsigned long long z[512] = {0};
+    unsigned long long z[768] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(snake::g_obsprof), z, sizeof z);
     return 0;
 }

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Timeline of one step's observation phase (diagnostic SNAKE_STAMPS build): s_memrealtime
-(100 MHz) at start/end of the first 128 queued resets and of every 512th
-env's encode block, relative to the earliest recorded start.
+(100 MHz) at start/end of the first 128 queued resets, of the first 128
+spawn-ahead jobs and of every 512th env's encode block, relative to the
+earliest recorded start.
 
     python scripts/obs_profile.py marl-snake_amd/build/libsnake_stamps.so
 """
@@ -27,7 +28,7 @@ def main():
     L.snake_debug_obsprof.argtypes = [ctypes.c_void_p]
     L.snake_debug_stamps.argtypes = [ctypes.c_void_p]
     st = np.zeros(72, dtype=np.uint64)
-    buf = np.zeros(512, dtype=np.uint64)
+    buf = np.zeros(768, dtype=np.uint64)
     g = torch.Generator(device='cuda').manual_seed(7)
     acts = torch.randint(0, 3, (300, N, 4), generator=g, device='cuda', dtype=torch.int8)
     v.reset()
@@ -46,6 +47,8 @@ def main():
         L.snake_debug_obsprof(buf.ctypes.data_as(ctypes.c_void_p))
         b = buf.astype(np.int64)
         rs, re_, es, ee = b[:128], b[128:256], b[256:384], b[384:512]
+        ss, se = b[512:640], b[640:768]
+        sok = (ss > 0) & (se > 0)
         nr = min(nres, 128)
         rs, re_ = rs[:nr], re_[:nr]
         ok = ee > 0
@@ -60,6 +63,9 @@ def main():
             'encode_start_us': pct(us(es[es > 0])),
             'encode_end_us': pct(us(ee[ok])),
             'encode_dur_us': pct((ee[ok] - es[ok]) / 100.0),
+            'spawn_start_us': pct(us(ss[sok])) if sok.any() else None,
+            'spawn_end_us': pct(us(se[sok])) if sok.any() else None,
+            'spawn_dur_us': pct((se[sok] - ss[sok]) / 100.0) if sok.any() else None,
         }), flush=True)
 
 
