@@ -16,7 +16,8 @@ exactly K steps between barrier + synchronize on both sides; value = all envs of
 all ranks x K / the slowest rank's time.
 
 A step is three kernels (include/snake_env.h snake_step): k_logic (rules, all
-envs), then k_autoreset (the step's auto-resets) concurrently with k_encode (the
+envs), then k_autoreset (the step's auto-resets, then the spawn-ahead attempts:
+next resets' permutations drawn early) concurrently with k_encode (the
 observations of every other env, on the library's side stream).
 
 The JSON line also carries:
