@@ -170,6 +170,44 @@ int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_en
 int snake_timing_enable(int on);
 int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
 
+/* ---- Fused consumer: the reference's DQN forward on the observation batch
+ * (train_dqn.py:104-151 DQN.forward / forward_features, train_ga.py:60-100),
+ * conv1 c->32, conv2 32->64, conv3 64->64 (3x3, pad 1, ReLU), NCHW flatten,
+ * fc1 64hw->256, fc2 256->128 (ReLU), fc3 128->A, on the bf16 matrix cores with
+ * fp32 accumulation (weights and activations rounded to bf16 between layers).
+ * obs: uint8 [B][h][w][c] (the env's NHWC per-snake observations, 0/1 values:
+ * the reference's /255 branch is not taken). h*w <= 144, w <= 16 (vision_range
+ * <= 5), c <= 32, A <= 4. */
+typedef struct {
+    int32_t height, width, channels, num_actions;
+} snake_dqn_cfg;
+
+typedef struct {        /* sizes for snake_dqn_forward (element counts) */
+    int64_t conv1_w;    /* bf16 [32][k1]: k = tap*cpad + channel, tap = ky*3 + kx, zero padded */
+    int64_t conv2_w;    /* bf16 [64][288]: k = tap*32 + channel */
+    int64_t conv3_w;    /* bf16 [64][576]: k = tap*64 + channel */
+    int64_t fc1_w;      /* bf16 [256][64*p16]: k = channel*p16 + y*w + x (zero for y*w+x >= h*w) */
+    int64_t fc2_w;      /* bf16 [128][256] */
+    int64_t act_per_obs;/* bf16 scratch per observation: 64*p16 */
+    int32_t cpad, p16, k1;   /* channels padded to a power of two >= 8; positions to 16; 9*cpad to 32 */
+    int32_t lds_conv;   /* LDS bytes per conv workgroup */
+} snake_dqn_layout;
+
+typedef struct {        /* device weights (layouts in snake_dqn_layout; biases and fc3 fp32) */
+    const uint16_t *conv1_w, *conv2_w, *conv3_w, *fc1_w, *fc2_w;
+    const float *conv1_b, *conv2_b, *conv3_b, *fc1_b, *fc2_b;
+    const float *fc3_w;  /* [A][128] */
+    const float *fc3_b;  /* [A] */
+} snake_dqn_net;
+
+int snake_dqn_plan(const snake_dqn_cfg *cfg, snake_dqn_layout *out);
+
+/* q_out: float [B][A]; feat_out (may be NULL): float [B][128] = forward_features;
+ * act_scratch: bf16 [B][act_per_obs] device buffer. Two launches on `stream`. */
+int snake_dqn_forward(const snake_dqn_cfg *cfg, const snake_dqn_net *net, const uint8_t *obs,
+                      int64_t batch, uint16_t *act_scratch, float *q_out, float *feat_out,
+                      void *stream);
+
 /* Last error message of this thread ("" if none). */
 const char *snake_last_error(void);
 

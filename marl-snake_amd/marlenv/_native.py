@@ -14,7 +14,8 @@ SNAKE_ABI_VERSION = 7
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
-           'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version')
+           'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version',
+           'snake_dqn_plan', 'snake_dqn_forward')
 
 
 class SnakeCfg(ctypes.Structure):
@@ -45,6 +46,22 @@ class SnakeState(ctypes.Structure):
 class SnakeOut(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
         'obs', 'rew', 'done', 'ep_done', 'rank', 'ep_stats', 'err')]
+
+
+class DqnCfg(ctypes.Structure):
+    _fields_ = [('height', ctypes.c_int32), ('width', ctypes.c_int32), ('channels', ctypes.c_int32),
+                ('num_actions', ctypes.c_int32)]
+
+
+class DqnLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ('conv1_w', 'conv2_w', 'conv3_w', 'fc1_w', 'fc2_w', 'act_per_obs')] + [
+        (n, ctypes.c_int32) for n in ('cpad', 'p16', 'k1', 'lds_conv')]
+
+
+class DqnNet(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        'conv1_w', 'conv2_w', 'conv3_w', 'fc1_w', 'fc2_w', 'conv1_b', 'conv2_b', 'conv3_b', 'fc1_b', 'fc2_b',
+        'fc3_w', 'fc3_b')]
 
 
 class NativeError(RuntimeError):
@@ -82,6 +99,8 @@ def lib(path=None):
     L.snake_step.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P,
                              ctypes.POINTER(SnakeOut), P]
     L.snake_render_rgb.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P, P, P]
+    L.snake_dqn_plan.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(DqnLayout)]
+    L.snake_dqn_forward.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(DqnNet), P, I64, P, P, P, P]
     L.snake_timing_enable.argtypes = [ctypes.c_int]
     L.snake_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_int64)]

@@ -1,0 +1,107 @@
+"""The fused DQN consumer (marl-snake_amd/csrc/dqn_kernels.hip) against a plain
+PyTorch fp32 restatement of the reference network (train_dqn.py:104-151).
+
+Tolerance: the matrix products take bf16 inputs (weights and activations are
+rounded to bf16 between layers, 8 significant bits) with fp32 accumulation, so
+outputs agree with the fp32 reference to |err| <= 2e-2 * max|ref| + 1e-3 (a
+bf16-emulating reference agrees to <= 2e-3 * max|ref|, which pins the layouts)."""
+import pytest
+
+torch = pytest.importorskip('torch')
+nn = torch.nn
+F = torch.nn.functional
+
+
+class RefDQN(nn.Module):
+    """train_dqn.py:104-151, restated (layers, flatten order, ReLUs)."""
+
+    def __init__(self, h, w, c, num_actions):
+        super().__init__()
+        self.conv1 = nn.Conv2d(c, 32, kernel_size=3, stride=1, padding=1)
+        self.conv2 = nn.Conv2d(32, 64, kernel_size=3, stride=1, padding=1)
+        self.conv3 = nn.Conv2d(64, 64, kernel_size=3, stride=1, padding=1)
+        self.fc1 = nn.Linear(h * w * 64, 256)
+        self.fc2 = nn.Linear(256, 128)
+        self.fc3 = nn.Linear(128, num_actions)
+
+    def forward_features(self, x, bf16=False):
+        r = (lambda t: t.to(torch.bfloat16).float()) if bf16 else (lambda t: t)
+        x = x.permute(0, 3, 1, 2).float()
+        x = x / 255.0 if x.max() > 1.0 else x
+        def lin(layer, t):
+            return F.linear(r(t), r(layer.weight), layer.bias)
+        def conv(layer, t):
+            return F.conv2d(r(t), r(layer.weight), layer.bias, padding=1)
+        x = F.relu(conv(self.conv1, x))
+        x = F.relu(conv(self.conv2, x))
+        x = F.relu(conv(self.conv3, x))
+        x = x.reshape(x.size(0), -1)
+        x = F.relu(lin(self.fc1, x))
+        return F.relu(lin(self.fc2, x))
+
+    def forward(self, x, bf16=False):
+        return F.linear(self.forward_features(x, bf16), self.fc3.weight, self.fc3.bias)
+
+
+def test_dqn_plan_sizes():
+    import ctypes
+    from marlenv import _native
+    lay = _native.DqnLayout()
+    cfg = _native.DqnCfg(11, 11, 8, 3)
+    assert _native.lib().snake_dqn_plan(ctypes.byref(cfg), ctypes.byref(lay)) == 0
+    assert (lay.cpad, lay.p16, lay.k1) == (8, 128, 96)
+    assert lay.fc1_w == 256 * 64 * 128 and lay.act_per_obs == 64 * 128
+    bad = _native.DqnCfg(20, 20, 8, 3)           # full 20x20 map: beyond this kernel's 144 positions
+    assert _native.lib().snake_dqn_plan(ctypes.byref(bad), ctypes.byref(lay)) == -1
+
+
+def _obs_batch(B, vr, fs, S=4, seed=0):
+    """Real observations: a short random rollout of the GPU env."""
+    from marlenv import SnakeVecEnv
+    n = max(1, -(-B // S))
+    v = SnakeVecEnv(n, num_snakes=S, seed=seed, height=20, width=20, vision_range=vr, frame_stack=fs)
+    v.reset()
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    for _ in range(12):
+        o, _, _, _ = v.step(torch.randint(0, 3, (n, S), generator=g, device='cuda', dtype=torch.int8))
+    return o.reshape(-1, *o.shape[2:])[:B].contiguous()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,vr,fs', [(512, 5, 1), (333, 5, 1), (64, 4, 2), (40, 3, 4), (1, 5, 1)])
+def test_dqn_forward_matches_fp32_reference(B, vr, fs):
+    from marlenv.dqn import DQNForward
+    torch.manual_seed(1)
+    h = w = 2 * vr + 1
+    c = 8 * fs
+    ref = RefDQN(h, w, c, 3).cuda()
+    obs = _obs_batch(B, vr, fs)
+    assert obs.shape == (B, h, w, c)
+    net = DQNForward(ref, h, w, c, 3)
+    q = net(obs)
+    feat = net.forward_features(obs)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        q32 = ref(obs)
+        f32 = ref.forward_features(obs)
+        qbf = ref(obs, bf16=True)
+    assert q.shape == (B, 3) and feat.shape == (B, 128)
+    assert torch.isfinite(q).all()
+    scale = float(q32.abs().max())
+    assert float((q - q32).abs().max()) <= 2e-2 * scale + 1e-3
+    assert float((q - qbf).abs().max()) <= 2e-3 * scale + 1e-4
+    fs_ = float(f32.abs().max())
+    assert float((feat - f32).abs().max()) <= 2e-2 * fs_ + 1e-3
+    # the argmax actions of a greedy policy agree wherever the reference's margin is clear
+    top2 = q32.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 0.05 * scale
+    assert bool((q.argmax(1)[clear] == q32.argmax(1)[clear]).all())
+
+
+@pytest.mark.gpu
+def test_dqn_rejects_non_uint8():
+    from marlenv.dqn import DQNForward
+    ref = RefDQN(11, 11, 8, 3).cuda()
+    net = DQNForward(ref, 11, 11, 8, 3)
+    with pytest.raises(TypeError):
+        net(torch.zeros((2, 11, 11, 8), device='cuda'))
