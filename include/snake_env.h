@@ -176,8 +176,8 @@ int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
  * fc1 64hw->256, fc2 256->128 (ReLU), fc3 128->A, on the bf16 matrix cores with
  * fp32 accumulation (weights and activations rounded to bf16 between layers).
  * obs: uint8 [B][h][w][c] (the env's NHWC per-snake observations, 0/1 values:
- * the reference's /255 branch is not taken). h*w <= 144, w <= 16 (vision_range
- * <= 5), c <= 32, A <= 4. */
+ * the reference's /255 branch is not taken). h = w = 2*vision_range+1 with
+ * vision_range in [1, 5], c = 8*frame_stack <= 32, A <= 4. */
 typedef struct {
     int32_t height, width, channels, num_actions;
 } snake_dqn_cfg;
@@ -186,7 +186,10 @@ typedef struct {        /* sizes for snake_dqn_forward (element counts) */
     int64_t conv1_w;    /* bf16 [32][k1]: k = tap*cpad + channel, tap = ky*3 + kx, zero padded */
     int64_t conv2_w;    /* bf16 [64][288]: k = tap*32 + channel */
     int64_t conv3_w;    /* bf16 [64][576]: k = tap*64 + channel */
-    int64_t fc1_w;      /* bf16 [256][64*p16]: k = channel*p16 + y*w + x (zero for y*w+x >= h*w) */
+    int64_t fc1_w;      /* bf16 [256][64*p16], k in conv3's MFMA fragment order:
+                         * k = m*1024 + half*512 + quad*128 + c16*8 + j*4 + r holds
+                         * channel (2*half + j)*16 + c16 at position p = m*16 + 4*quad + r
+                         * (p = y*w + x; zero weights for p >= h*w) */
     int64_t fc2_w;      /* bf16 [128][256] */
     int64_t act_per_obs;/* bf16 scratch per observation: 64*p16 */
     int32_t cpad, p16, k1;   /* channels padded to a power of two >= 8; positions to 16; 9*cpad to 32 */

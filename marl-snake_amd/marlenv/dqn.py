@@ -66,14 +66,20 @@ class DQNForward:
         fc1 = g('fc1.weight')
         if tuple(fc1.shape) != (256, 64 * P):
             raise ValueError('fc1.weight shape %s != (256, %d)' % (tuple(fc1.shape), 64 * P))
-        fc1p = torch.zeros((256, 64, P16), **f32)
-        fc1p[:, :, :P] = fc1.reshape(256, 64, P)             # NCHW flatten: ch * h*w + y*w + x
+        # k in conv3's fragment order (snake_env.h snake_dqn_layout.fc1_w) -> the
+        # reference's NCHW flatten index channel * h*w + y*w + x
+        k = torch.arange(64 * P16, device=d)
+        r, j, c16, quad = k % 4, (k // 4) % 2, (k // 8) % 16, (k // 128) % 4
+        half, m = (k // 512) % 2, k // 1024
+        ch, p = (2 * half + j) * 16 + c16, m * 16 + 4 * quad + r
+        src = torch.where(p < P, ch * P + p, 0)
+        fc1p = torch.where((p < P)[None, :], fc1[:, src], torch.zeros((), **f32))
         fc3 = g('fc3.weight')
         if tuple(fc3.shape) != (A, 128):
             raise ValueError('fc3.weight shape %s != (%d, 128)' % (tuple(fc3.shape), A))
         self.tensors = dict(
             conv1_w=conv_pack(w1, CP, K1), conv2_w=conv_pack(w2, 32, 288), conv3_w=conv_pack(w3, 64, 576),
-            fc1_w=bits(fc1p.reshape(256, 64 * P16)), fc2_w=bits(g('fc2.weight')),
+            fc1_w=bits(fc1p), fc2_w=bits(g('fc2.weight')),
             conv1_b=g('conv1.bias'), conv2_b=g('conv2.bias'), conv3_b=g('conv3.bias'),
             fc1_b=g('fc1.bias'), fc2_b=g('fc2.bias'), fc3_w=fc3.contiguous(), fc3_b=g('fc3.bias'))
         for k, n in (('conv1_w', lay.conv1_w), ('conv2_w', lay.conv2_w), ('conv3_w', lay.conv3_w),

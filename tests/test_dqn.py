@@ -51,8 +51,10 @@ def test_dqn_plan_sizes():
     assert _native.lib().snake_dqn_plan(ctypes.byref(cfg), ctypes.byref(lay)) == 0
     assert (lay.cpad, lay.p16, lay.k1) == (8, 128, 96)
     assert lay.fc1_w == 256 * 64 * 128 and lay.act_per_obs == 64 * 128
-    bad = _native.DqnCfg(20, 20, 8, 3)           # full 20x20 map: beyond this kernel's 144 positions
+    bad = _native.DqnCfg(20, 20, 8, 3)           # full 20x20 map: vision_range <= 5 only
     assert _native.lib().snake_dqn_plan(ctypes.byref(bad), ctypes.byref(lay)) == -1
+    for h, w, c, a in ((11, 9, 8, 3), (11, 11, 12, 3), (11, 11, 40, 3), (11, 11, 8, 5), (4, 4, 8, 3)):
+        assert _native.lib().snake_dqn_plan(ctypes.byref(_native.DqnCfg(h, w, c, a)), ctypes.byref(lay)) == -1
 
 
 def _obs_batch(B, vr, fs, S=4, seed=0):
@@ -68,7 +70,8 @@ def _obs_batch(B, vr, fs, S=4, seed=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('B,vr,fs', [(512, 5, 1), (333, 5, 1), (64, 4, 2), (40, 3, 4), (1, 5, 1)])
+@pytest.mark.parametrize('B,vr,fs', [(512, 5, 1), (333, 5, 1), (64, 4, 2), (40, 3, 4), (1, 5, 1),
+                                     (257, 2, 1), (100, 1, 3), (3000, 5, 2)])
 def test_dqn_forward_matches_fp32_reference(B, vr, fs):
     from marlenv.dqn import DQNForward
     torch.manual_seed(1)
