@@ -188,11 +188,12 @@ typedef struct {        /* sizes for snake_dqn_forward (element counts) */
     int64_t conv3_w;    /* bf16 [64][576]: k = tap*64 + channel */
     int64_t fc1_w;      /* bf16 [256][64*p16], k in conv3's MFMA fragment order:
                          * k = m*1024 + half*512 + quad*128 + c16*8 + j*4 + r holds
-                         * channel (2*half + j)*16 + c16 at position p = m*16 + 4*quad + r
-                         * (p = y*w + x; zero weights for p >= h*w) */
+                         * channel (2*half + j)*16 + c16 at GEMM row i = m*16 + 4*quad + r,
+                         * i.e. at observation position snake_dqn_rows()[i] (zero weights
+                         * where that is -1) */
     int64_t fc2_w;      /* bf16 [128][256] */
     int64_t act_per_obs;/* bf16 scratch per observation: 64*p16 */
-    int32_t cpad, p16, k1;   /* channels padded to a power of two >= 8; positions to 16; 9*cpad to 32 */
+    int32_t cpad, p16, k1;   /* channels padded to a power of two >= 8; GEMM rows (16 per tile); 9*cpad to 32 */
     int32_t lds_conv;   /* LDS bytes per conv workgroup */
 } snake_dqn_layout;
 
@@ -204,6 +205,12 @@ typedef struct {        /* device weights (layouts in snake_dqn_layout; biases a
 } snake_dqn_net;
 
 int snake_dqn_plan(const snake_dqn_cfg *cfg, snake_dqn_layout *out);
+
+/* The convolutions' GEMM row -> observation position map (p = y*w + x, -1 for a
+ * padding row): rows[i] for i < p16. Rows are assigned so that the 16 rows of a
+ * tile sit in distinct LDS banks (dqn_kernels.hip). Returns p16 (rows may be
+ * NULL to query it), < 0 on error. */
+int64_t snake_dqn_rows(const snake_dqn_cfg *cfg, int32_t *rows, int64_t n);
 
 /* q_out: float [B][A]; feat_out (may be NULL): float [B][128] = forward_features;
  * act_scratch: bf16 [B][act_per_obs] device buffer. Two launches on `stream`. */

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -56,33 +57,61 @@ __device__ __forceinline__ void wave_lds_sync()
 
 // ---- k_dqn_conv ---------------------------------------------------------
 // A workgroup of two waves runs one observation at a time through the three
-// convolutions. The layer images live in LDS as NHWC bf16 with a zero border
-// ((h+2) x (w+2) positions; a position's channels padded by 16 bytes so the 16
-// lanes of one ds_read_b128 group hit distinct banks): the A fragment of tap
-// (dy, dx) at output row p is one 16-byte read at a fixed offset from the row's
-// own position, with no bounds checks, and with h, w and the channel counts
-// compile-time that offset is an immediate. Each wave computes half the output
-// channels (B fragments = weights from global memory, shared through L1/L2 by
-// every workgroup) for all position tiles, so each A fragment feeds two MFMAs.
+// convolutions. Each layer's image lives in LDS as bf16 with a zero border
+// ((h+2) x (w+2) positions q), chunk-major: 8 channels of one position = one
+// 16-byte cell at chunk * R*16 + q*16 (R = positions rounded up to 16). The A
+// fragment of tap (dy, dx) at GEMM row i is then one 16-byte read at a fixed
+// offset from the row's own cell: no bounds checks, and with h, w and the
+// channel counts compile-time the offset is an immediate. GEMM rows are
+// assigned to positions so that the 16 rows of a tile have distinct q mod 16
+// (row r of tile t = the t-th position with q % 16 == r): the lanes of every
+// ds_read_b128 lane group then hit distinct banks for every tap. Each wave
+// computes half the output channels (B fragments = weights, read from global
+// memory through L1/L2 by every workgroup) for all row tiles, so each A
+// fragment feeds NTW MFMAs.
+__host__ __device__ constexpr int dqn_bidx(int p, int W) { return (p / W + 1) * (W + 2) + p % W + 1; }
+
+// GEMM row (tile * 16 + q % 16) of observation position p
+__host__ __device__ constexpr int dqn_row_of(int p, int W)
+{
+    const int r = dqn_bidx(p, W) & 15;
+    int t = 0;
+    for (int p2 = 0; p2 < p; p2++) t += (dqn_bidx(p2, W) & 15) == r;
+    return t * 16 + r;
+}
+
+__host__ __device__ constexpr int dqn_tiles(int W)
+{
+    int mt = (W * W + 15) / 16;
+    for (int p = 0; p < W * W; p++) {
+        const int t = dqn_row_of(p, W) / 16 + 1;
+        mt = t > mt ? t : mt;
+    }
+    return mt;
+}
+
 template <int VR, int CL>
 struct Geo {
     static constexpr int W = 2 * VR + 1, H = W, P = H * W;
-    static constexpr int MT = (P + 15) / 16, P16 = MT * 16;
+    static constexpr int MT = dqn_tiles(W), P16 = MT * 16;
     static constexpr int BW = W + 2, NB = BW * (H + 2);
     static constexpr int CP = 1 << CL;
-    static constexpr int S0 = 2 * CP + (CP >= 16 ? 16 : 0);   // bytes per position: input image
-    static constexpr int S1 = 2 * 32 + 16, S2 = 2 * 64 + 16;   // conv1 / conv2 output images
+    static constexpr int CH = ((NB + 15) / 16) * 16 * 16;       // bytes per 8-channel chunk plane
     static constexpr int K1S = (9 * CP + 31) / 32;              // conv1 k steps
-    static constexpr int OFF1 = 0;                              // a1 [NB][S1]
-    static constexpr int OFF2 = NB * S1;                        // a2 [NB][S2]; a0 [NB][S0] overlays it
-    static constexpr int OFFT = OFF2 + NB * S2;                 // u16 [P16]: border index of row p
+    static constexpr int OFF1 = 0;                              // a1: 4 planes
+    static constexpr int OFF2 = 4 * CH;                         // a2: 8 planes; a0 (CP/8 planes) overlays it
+    static constexpr int OFFT = OFF2 + 8 * CH;                  // u16 [P16]: border index of GEMM row, 0xffff pad
     static constexpr int LDS = OFFT + P16 * 2;
     static constexpr int NCELL0 = NB * CP / 8;                  // 16-byte cells of the input image
-    static constexpr int NC = (NCELL0 + 127) / 128;             // per thread
-    static constexpr int CENTER = (H / 2 + 1) * BW + W / 2 + 1;
     static constexpr int NBORDER = NB - P;
-    __host__ __device__ static constexpr int bidx(int p) { return (p / W + 1) * BW + p % W + 1; }
-    __host__ __device__ static constexpr int tapoff(int tap, int S) { return ((tap / 3) * BW + tap % 3) * S; }
+    __host__ __device__ static constexpr int tapoff(int tap) { return ((tap / 3) * BW + tap % 3) * 16; }
+    // gather position of a padding row with q % 16 == r (finite values, results unused)
+    __host__ __device__ static constexpr int padq(int r)
+    {
+        for (int q = BW + 1; q < NB - BW - 1; q++)
+            if ((q & 15) == r) return q;
+        return (H / 2 + 1) * BW + W / 2 + 1;
+    }
 };
 
 __device__ __forceinline__ uint32_t pack2(float lo, float hi)
@@ -108,11 +137,12 @@ __device__ __forceinline__ u32x4 bytes_to_bf16(uint2 v)
 }
 
 // One 3x3 convolution of the workgroup's observation, this wave's NTW output
-// channel tiles starting at tile nt0. src / S: input border image and its
-// position stride; tap offsets: per k step either compile-time (CIN >= 32: one
-// tap per k step, the lane's 8 channels at 2 * kq bytes) or the lane's
-// precomputed toff[ks], channel included (conv1 with CIN < 32).
-template <int VR, int CL, int S, int CIN, int KS, int NTW>
+// channel tiles starting at tile nt0, from the chunk-major image at src.
+// gpos[m] = byte offset of the lane's row cell minus one row and one column,
+// plus the lane's chunk (quad) plane. Tap offsets per k step: compile-time for
+// CIN >= 32 (one tap per k step), else the lane's precomputed toff[ks] (conv1
+// with CIN < 32: chunk included, the quad plane taken back out).
+template <int VR, int CL, int CIN, int KS, int NTW, int COUT>
 __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int *gpos, const int *toff,
                                          const uint16_t *__restrict__ wt, int nt0, int lane,
                                          f32x4 (&acc)[Geo<VR, CL>::MT][NTW])
@@ -120,50 +150,81 @@ __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int 
     using G = Geo<VR, CL>;
     const int r16 = lane & 15, kq = 8 * (lane >> 4);
     constexpr int K = KS * 32;
-    int abase[G::MT];
+    // weights through a buffer descriptor: the lane's offset in one VGPR, the
+    // (tile, k step) part a scalar offset -- no per-load 64-bit addresses
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(wt), 0, 2 * K * COUT, 0x00020000);
+    const int voff = 2 * ((nt0 * 16 + r16) * K + kq);
+    auto load_b = [&](bf16x8 (&bw)[NTW], int ks) {
 #pragma unroll
-    for (int m = 0; m < G::MT; m++) abase[m] = src + (gpos[m] - G::BW - 1) * S + (CIN >= 32 ? 2 * kq : 0);
+        for (int j = 0; j < NTW; j++) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (j * 16 * K + ks * 32), 0);
+            bw[j] = __builtin_bit_cast(bf16x8, v);
+        }
+    };
 #pragma unroll
     for (int m = 0; m < G::MT; m++)
 #pragma unroll
         for (int j = 0; j < NTW; j++) acc[m][j] = (f32x4)0.0f;
-    const uint16_t *wrow = wt + (nt0 * 16 + r16) * K + kq;
+    auto a_off = [&](int ks) {
+        if constexpr (CIN >= 32) return G::tapoff((ks * 32) / CIN) + ((ks * 32) % CIN) / 8 * G::CH;
+        else return toff[ks];
+    };
+    // B one k step ahead; A (the MT fragments of a k step) one k step ahead when
+    // ABUF == 2 (one wave per SIMD: nothing else hides the LDS latency)
+    constexpr int ABUF = NTW >= 4 ? 2 : 1;
+    bf16x8 bcur[NTW], bnxt[NTW];
+    bf16x8 abuf[ABUF][G::MT];
+    load_b(bcur, 0);
+    if constexpr (ABUF == 2) {
+#pragma unroll
+        for (int m = 0; m < G::MT; m++) abuf[0][m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(0));
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
-        bf16x8 bw[NTW];
+        if (ks + 1 < KS) load_b(bnxt, ks + 1);
+        bf16x8 *av = abuf[ABUF == 2 ? (ks & 1) : 0];
+        if constexpr (ABUF == 2) {
+            if (ks + 1 < KS) {
 #pragma unroll
-        for (int j = 0; j < NTW; j++) bw[j] = *reinterpret_cast<const bf16x8 *>(wrow + j * 16 * K + ks * 32);
-        int off;
-        if constexpr (CIN >= 32) off = G::tapoff((ks * 32) / CIN, S) + 2 * ((ks * 32) % CIN);
-        else off = toff[ks];
+                for (int m = 0; m < G::MT; m++)
+                    abuf[(ks + 1) & 1][m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(ks + 1));
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < G::MT; m++) av[m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(ks));
+        }
 #pragma unroll
         for (int m = 0; m < G::MT; m++) {
-            const bf16x8 av = *reinterpret_cast<const bf16x8 *>(lds + abase[m] + off);
 #pragma unroll
-            for (int j = 0; j < NTW; j++) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bw[j], acc[m][j], 0, 0, 0);
+            for (int j = 0; j < NTW; j++) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], bcur[j], acc[m][j], 0, 0, 0);
+        }
+        if (ks + 1 < KS) {
+#pragma unroll
+            for (int j = 0; j < NTW; j++) bcur[j] = bnxt[j];
         }
     }
 }
 
-// bias + ReLU -> bf16 into the interior of an NHWC border image (stride SD)
-template <int VR, int CL, int SD, int NTW>
+// bias + ReLU -> bf16 into the interior of a chunk-major border image
+template <int VR, int CL, int NTW>
 __device__ __forceinline__ void conv_store_lds(uint8_t *lds, int dst, const uint16_t *ptab, int nt0, int lane,
-                                               const float *__restrict__ bias, f32x4 (&acc)[Geo<VR, CL>::MT][NTW])
+                                               const float (&bias)[NTW], f32x4 (&acc)[Geo<VR, CL>::MT][NTW])
 {
     using G = Geo<VR, CL>;
     const int r16 = lane & 15, quad = lane >> 4;
 #pragma unroll
     for (int j = 0; j < NTW; j++) {
         const int co = (nt0 + j) * 16 + r16;
-        const float bb = bias[co];
+        const float bb = bias[j];
+        const int cbase = dst + (co >> 3) * G::CH + 2 * (co & 7);
 #pragma unroll
         for (int m = 0; m < G::MT; m++) {
             const uint2 pq = *reinterpret_cast<const uint2 *>(ptab + m * 16 + 4 * quad);
             const uint32_t q[4] = {pq.x & 0xffffu, pq.x >> 16, pq.y & 0xffffu, pq.y >> 16};
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                if (m < G::MT - 1 || q[r] != 0xffffu)
-                    *reinterpret_cast<uint16_t *>(lds + dst + q[r] * SD + 2 * co) =
+                if (q[r] != 0xffffu)
+                    *reinterpret_cast<uint16_t *>(lds + cbase + q[r] * 16) =
                         (uint16_t)bf16_bits(fmaxf(acc[m][j][r] + bb, 0.0f));
             }
         }
@@ -179,94 +240,127 @@ struct ConvArgs {
     uint16_t *act;                      // [B][64 * P16], k order: snake_dqn_layout.fc1_w
 };
 
-template <int VR, int CL>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) k_dqn_conv(const ConvArgs a)
+template <int NW>
+__device__ __forceinline__ void conv_sync()
+{
+    if constexpr (NW == 1) wave_lds_sync();
+    else __syncthreads();
+}
+
+// NW waves per observation (1: no workgroup barriers, all four channel tiles of
+// conv2/conv3 per wave, each A fragment feeding four MFMAs; 2: two waves split
+// the channel tiles).
+template <int VR, int CL, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 1 ? 1 : 2))) k_dqn_conv(const ConvArgs a)
 {
     using G = Geo<VR, CL>;
+    constexpr int NT = 64 * NW;
+    constexpr int NC = (G::NCELL0 + NT - 1) / NT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[G::LDS];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r16 = lane & 15, kq = 8 * (lane >> 4);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform
+    const int r16 = lane & 15;
     uint16_t *ptab = reinterpret_cast<uint16_t *>(lds + G::OFFT);
-    for (int p = tid; p < G::P16; p += 128) ptab[p] = p < G::P ? (uint16_t)G::bidx(p) : (uint16_t)0xffffu;
-    for (int i = tid; i < G::NB * G::S1 / 16; i += 128) reinterpret_cast<u32x4 *>(lds + G::OFF1)[i] = (u32x4)0u;
-    // gather rows (padding rows read the centre: finite values, results unused)
+    for (int i = tid; i < G::P16; i += NT) ptab[i] = (uint16_t)0xffffu;
+    for (int i = tid; i < 4 * G::CH / 16; i += NT) reinterpret_cast<u32x4 *>(lds + G::OFF1)[i] = (u32x4)0u;
+    conv_sync<NW>();
+    for (int p = tid; p < G::P; p += NT) ptab[dqn_row_of(p, G::W)] = (uint16_t)dqn_bidx(p, G::W);
+    conv_sync<NW>();
+    const int qplane = (lane >> 4) * G::CH;
     int gpos[G::MT];
 #pragma unroll
     for (int m = 0; m < G::MT; m++) {
-        const int p = m * 16 + r16;
-        gpos[m] = p < G::P ? G::bidx(p) : G::CENTER;
+        const int q = ptab[m * 16 + r16];
+        gpos[m] = ((q != 0xffff ? q : G::padq(r16)) - G::BW - 1) * 16 + qplane;
     }
     // conv1 per-lane tap offsets (k = tap * CP + channel; taps past the 9th meet zero weights)
     int toff1[G::K1S];
 #pragma unroll
     for (int ks = 0; ks < G::K1S; ks++) {
-        const int k0 = ks * 32 + kq, tap = k0 >> CL, ci = k0 & (G::CP - 1);
-        toff1[ks] = tap < 9 ? G::tapoff(tap, G::S0) + 2 * ci : G::tapoff(4, G::S0);
+        const int k0 = ks * 32 + 8 * (lane >> 4), tap = k0 >> CL, ci = k0 & (G::CP - 1);
+        toff1[ks] = (tap < 9 ? G::tapoff(tap) : G::tapoff(4)) + (ci >> 3) * G::CH - qplane;
     }
-    // input cells of this thread: source byte offset within the observation, or -1 (zero)
-    int csrc[G::NC], cdst[G::NC];
+    // input cells of this thread (cell c: chunk c / NB, position c % NB): source
+    // byte offset within the observation, or -1 (zero)
+    int csrc[NC], cdst[NC];
 #pragma unroll
-    for (int i = 0; i < G::NC; i++) {
-        const int c = tid + 128 * i;
-        const int q = c / (G::CP / 8), g = c % (G::CP / 8);
+    for (int i = 0; i < NC; i++) {
+        const int c = tid + NT * i;
+        const int g = c / G::NB, q = c % G::NB;
         const int y = q / G::BW - 1, x = q % G::BW - 1;
         const bool in = c < G::NCELL0 && (unsigned)y < (unsigned)G::H && (unsigned)x < (unsigned)G::W && g * 8 < a.C;
         csrc[i] = in ? (y * G::W + x) * a.C + g * 8 : -1;
-        cdst[i] = c < G::NCELL0 ? G::OFF2 + q * G::S0 + g * 16 : -1;
+        cdst[i] = c < G::NCELL0 ? G::OFF2 + g * G::CH + q * 16 : -1;
     }
-    uint2 xin[G::NC];
+    uint2 xin[NC];
     auto load_obs = [&](int64_t b) {
         const uint8_t *x = a.obs + b * (int64_t)(G::P * a.C);
 #pragma unroll
-        for (int i = 0; i < G::NC; i++) xin[i] = csrc[i] >= 0 ? *reinterpret_cast<const uint2 *>(x + csrc[i]) : make_uint2(0, 0);
+        for (int i = 0; i < NC; i++) xin[i] = csrc[i] >= 0 ? *reinterpret_cast<const uint2 *>(x + csrc[i]) : make_uint2(0, 0);
     };
+    constexpr int NT1 = 2 / NW, NT3 = 4 / NW;
+    // biases of this lane's output channels, loaded once
+    float bias1[NT1], bias2[NT3], bias3[NT3];
+#pragma unroll
+    for (int j = 0; j < NT1; j++) bias1[j] = a.b1[(w * NT1 + j) * 16 + r16];
+#pragma unroll
+    for (int j = 0; j < NT3; j++) {
+        bias2[j] = a.b2[(w * NT3 + j) * 16 + r16];
+        bias3[j] = a.b3[(w * NT3 + j) * 16 + r16];
+    }
     int64_t b = blockIdx.x;
     if (b < a.B) load_obs(b);
-    __syncthreads();
     for (; b < a.B; b += gridDim.x) {
         // input image (whole, border included) over the a2 area
 #pragma unroll
-        for (int i = 0; i < G::NC; i++)
+        for (int i = 0; i < NC; i++)
             if (cdst[i] >= 0) *reinterpret_cast<u32x4 *>(lds + cdst[i]) = bytes_to_bf16(xin[i]);
+#ifndef DQN_EXPT_NO_XIN
         if (b + gridDim.x < a.B) load_obs(b + gridDim.x);
-        __syncthreads();
-        {   // conv1: CP -> 32, wave w: channel tile w
-            f32x4 acc[G::MT][1];
-            conv_mma<VR, CL, G::S0, G::CP, G::K1S, 1>(lds, G::OFF2, gpos, toff1, a.w1, w, lane, acc);
-            conv_store_lds<VR, CL, G::S1, 1>(lds, G::OFF1, ptab, w, lane, a.b1, acc);
+#endif
+        conv_sync<NW>();
+        {   // conv1: CP -> 32
+            f32x4 acc[G::MT][NT1];
+            conv_mma<VR, CL, G::CP, G::K1S, NT1, 32>(lds, G::OFF2, gpos, toff1, a.w1, w * NT1, lane, acc);
+            conv_store_lds<VR, CL, NT1>(lds, G::OFF1, ptab, w * NT1, lane, bias1, acc);
         }
-        __syncthreads();
+        conv_sync<NW>();
         // the input image is dead: restore a2's zero border
-        for (int i = tid; i < G::NBORDER * 8; i += 128) {
-            const int bi = i >> 3, part = i & 7;
+        for (int i = tid; i < G::NBORDER * 8; i += NT) {
+            const int bi = i >> 3, chunk = i & 7;
             int q;
             if (bi < G::BW) q = bi;
             else if (bi < 2 * G::BW) q = (G::H + 1) * G::BW + bi - G::BW;
             else q = (1 + ((bi - 2 * G::BW) >> 1)) * G::BW + ((bi - 2 * G::BW) & 1) * (G::BW - 1);
-            *reinterpret_cast<u32x4 *>(lds + G::OFF2 + q * G::S2 + part * 16) = (u32x4)0u;
+            *reinterpret_cast<u32x4 *>(lds + G::OFF2 + chunk * G::CH + q * 16) = (u32x4)0u;
         }
-        {   // conv2: 32 -> 64, wave w: channel tiles 2w, 2w+1
-            f32x4 acc[G::MT][2];
-            conv_mma<VR, CL, G::S1, 32, 9, 2>(lds, G::OFF1, gpos, nullptr, a.w2, 2 * w, lane, acc);
-            conv_store_lds<VR, CL, G::S2, 2>(lds, G::OFF2, ptab, 2 * w, lane, a.b2, acc);
+        {   // conv2: 32 -> 64
+            f32x4 acc[G::MT][NT3];
+            conv_mma<VR, CL, 32, 9, NT3, 64>(lds, G::OFF1, gpos, nullptr, a.w2, w * NT3, lane, acc);
+            conv_store_lds<VR, CL, NT3>(lds, G::OFF2, ptab, w * NT3, lane, bias2, acc);
         }
-        __syncthreads();
-        {   // conv3: 64 -> 64 -> global, in MFMA fragment order (k = m*1024 + w*512 + lane*8 + j*4 + r)
-            f32x4 acc[G::MT][2];
-            conv_mma<VR, CL, G::S2, 64, 18, 2>(lds, G::OFF2, gpos, nullptr, a.w3, 2 * w, lane, acc);
-            const float b0 = a.b3[(2 * w) * 16 + r16], b1 = a.b3[(2 * w + 1) * 16 + r16];
-            u32x4 *dst = reinterpret_cast<u32x4 *>(a.act + b * (int64_t)(64 * G::P16)) + w * 64 + lane;
+        conv_sync<NW>();
+        {   // conv3: 64 -> 64 -> global, in MFMA fragment order
+            // (k = m*1024 + half*512 + lane*8 + j*4 + r, channel tile 2*half + j)
+            f32x4 acc[G::MT][NT3];
+            conv_mma<VR, CL, 64, 18, NT3, 64>(lds, G::OFF2, gpos, nullptr, a.w3, w * NT3, lane, acc);
+            u32x4 *dst = reinterpret_cast<u32x4 *>(a.act + b * (int64_t)(64 * G::P16)) + lane;
 #pragma unroll
-            for (int m = 0; m < G::MT; m++) {
-                u32x4 v;
-                v[0] = pack2(fmaxf(acc[m][0][0] + b0, 0.0f), fmaxf(acc[m][0][1] + b0, 0.0f));
-                v[1] = pack2(fmaxf(acc[m][0][2] + b0, 0.0f), fmaxf(acc[m][0][3] + b0, 0.0f));
-                v[2] = pack2(fmaxf(acc[m][1][0] + b1, 0.0f), fmaxf(acc[m][1][1] + b1, 0.0f));
-                v[3] = pack2(fmaxf(acc[m][1][2] + b1, 0.0f), fmaxf(acc[m][1][3] + b1, 0.0f));
-                dst[m * 128] = v;
+            for (int h = 0; h < NT3 / 2; h++) {
+                const int half = w * (NT3 / 2) + h;
+                const float b0 = bias3[2 * h], b1 = bias3[2 * h + 1];
+#pragma unroll
+                for (int m = 0; m < G::MT; m++) {
+                    u32x4 v;
+                    v[0] = pack2(fmaxf(acc[m][2 * h][0] + b0, 0.0f), fmaxf(acc[m][2 * h][1] + b0, 0.0f));
+                    v[1] = pack2(fmaxf(acc[m][2 * h][2] + b0, 0.0f), fmaxf(acc[m][2 * h][3] + b0, 0.0f));
+                    v[2] = pack2(fmaxf(acc[m][2 * h + 1][0] + b1, 0.0f), fmaxf(acc[m][2 * h + 1][1] + b1, 0.0f));
+                    v[3] = pack2(fmaxf(acc[m][2 * h + 1][2] + b1, 0.0f), fmaxf(acc[m][2 * h + 1][3] + b1, 0.0f));
+                    dst[m * 128 + half * 64] = v;
+                }
             }
         }
-        __syncthreads();
+        conv_sync<NW>();
     }
 }
 
@@ -289,13 +383,14 @@ struct FcArgs {
 // written after the stage's MFMAs, one barrier per stage), each B fragment read
 // from LDS feeds two MFMAs (the wave's two row tiles); the A fragments (the
 // conv3 activations) are loaded straight to registers a stage ahead. Tile image:
-// [k32 plane][n][4 x 16 B], chunk c of row n stored at c ^ ((n >> 2) & 3) so
-// the 16 rows of one ds_read_b128 lane group hit distinct banks.
+// [k32 plane][n][4 x 16 B], chunk c of row n stored at c ^ ((n >> 2) & 2): the
+// 16 lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, ...) then hit
+// distinct banks.
 constexpr int kFcRowsPerWave = 32;
 
 __device__ __forceinline__ int fc_tile_off(int plane, int n, int c)
 {
-    return plane * 16384 + n * 64 + ((c ^ ((n >> 2) & 3)) << 4);
+    return plane * 16384 + n * 64 + ((c ^ ((n >> 2) & 2)) << 4);
 }
 
 __global__ void __launch_bounds__(512) k_dqn_fc(const FcArgs a)
@@ -456,16 +551,30 @@ using namespace snake::dqn;
 
 namespace {
 typedef void (*conv_kernel_t)(ConvArgs);
-template <int VR, int CL>
-constexpr conv_kernel_t conv_kernel() { return k_dqn_conv<VR, CL>; }
-const conv_kernel_t kConvKernels[5][3] = {
-    {conv_kernel<1, 3>(), conv_kernel<1, 4>(), conv_kernel<1, 5>()},
-    {conv_kernel<2, 3>(), conv_kernel<2, 4>(), conv_kernel<2, 5>()},
-    {conv_kernel<3, 3>(), conv_kernel<3, 4>(), conv_kernel<3, 5>()},
-    {conv_kernel<4, 3>(), conv_kernel<4, 4>(), conv_kernel<4, 5>()},
-    {conv_kernel<5, 3>(), conv_kernel<5, 4>(), conv_kernel<5, 5>()},
+template <int NW>
+struct ConvTable {
+    conv_kernel_t k[5][3] = {
+        {k_dqn_conv<1, 3, NW>, k_dqn_conv<1, 4, NW>, k_dqn_conv<1, 5, NW>},
+        {k_dqn_conv<2, 3, NW>, k_dqn_conv<2, 4, NW>, k_dqn_conv<2, 5, NW>},
+        {k_dqn_conv<3, 3, NW>, k_dqn_conv<3, 4, NW>, k_dqn_conv<3, 5, NW>},
+        {k_dqn_conv<4, 3, NW>, k_dqn_conv<4, 4, NW>, k_dqn_conv<4, 5, NW>},
+        {k_dqn_conv<5, 3, NW>, k_dqn_conv<5, 4, NW>, k_dqn_conv<5, 5, NW>},
+    };
 };
-int g_conv_grid[5][3];
+const ConvTable<1> kConv1;
+const ConvTable<2> kConv2;
+int g_conv_grid[2][5][3];
+// waves per observation in k_dqn_conv: SNAKE_DQN_WAVES=1|2 (default 2; one wave
+// per observation measured 35 % slower: nothing hides its LDS / L2 latencies)
+int conv_waves()
+{
+    static int nw = 0;
+    if (!nw) {
+        const char *e = getenv("SNAKE_DQN_WAVES");
+        nw = (e && atoi(e) == 1) ? 1 : 2;
+    }
+    return nw;
+}
 }  // namespace
 
 extern "C" int snake_dqn_plan(const snake_dqn_cfg *cfg, snake_dqn_layout *out)
@@ -483,7 +592,7 @@ extern "C" int snake_dqn_plan(const snake_dqn_cfg *cfg, snake_dqn_layout *out)
     if (A < 1 || A > 4) { set_error("snake_dqn: num_actions must be in [1, 4] (got %d)", A); return SNAKE_E_CONFIG; }
     int cl = 3;
     while ((1 << cl) < C) cl++;
-    const int MT = (H * W + 15) / 16, P16 = MT * 16, CP = 1 << cl;
+    const int MT = dqn_tiles(W), P16 = MT * 16, CP = 1 << cl;
     const int NB = (H + 2) * (W + 2);
     out->cpad = CP;
     out->p16 = P16;
@@ -494,8 +603,21 @@ extern "C" int snake_dqn_plan(const snake_dqn_cfg *cfg, snake_dqn_layout *out)
     out->fc1_w = 256ll * 64 * P16;
     out->fc2_w = 128ll * 256;
     out->act_per_obs = 64ll * P16;
-    out->lds_conv = (int32_t)(NB * (80 + 144) + 2 * P16);
+    out->lds_conv = (int32_t)(12 * ((NB + 15) / 16) * 256 + 2 * P16);
     return SNAKE_OK;
+}
+
+extern "C" int64_t snake_dqn_rows(const snake_dqn_cfg *cfg, int32_t *rows, int64_t n)
+{
+    snake_dqn_layout lay;
+    const int rc = snake_dqn_plan(cfg, &lay);
+    if (rc) return rc;
+    if (rows) {
+        if (n < lay.p16) { set_error("snake_dqn_rows: need %d entries", lay.p16); return SNAKE_E_ARG; }
+        for (int i = 0; i < lay.p16; i++) rows[i] = -1;
+        for (int p = 0; p < cfg->height * cfg->width; p++) rows[dqn_row_of(p, cfg->width)] = p;
+    }
+    return lay.p16;
 }
 
 extern "C" int snake_dqn_forward(const snake_dqn_cfg *cfg, const snake_dqn_net *net, const uint8_t *obs,
@@ -520,20 +642,22 @@ extern "C" int snake_dqn_forward(const snake_dqn_cfg *cfg, const snake_dqn_net *
     ca.b1 = net->conv1_b; ca.b2 = net->conv2_b; ca.b3 = net->conv3_b;
     ca.act = act_scratch;
     const int vi = (cfg->height - 3) / 2, ci = lay.cpad == 8 ? 0 : (lay.cpad == 16 ? 1 : 2);
-    const conv_kernel_t kc = kConvKernels[vi][ci];
-    if (!g_conv_grid[vi][ci]) {   // persistent grid: the resident workgroups of the whole device
+    const int nw = conv_waves();
+    const conv_kernel_t kc = nw == 1 ? kConv1.k[vi][ci] : kConv2.k[vi][ci];
+    int &grid = g_conv_grid[nw - 1][vi][ci];
+    if (!grid) {   // persistent grid: the resident workgroups of the whole device
         int per_cu = 0, dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kc, 128, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kc, 64 * nw, 0) != hipSuccess ||
             per_cu < 1 || cus < 1) {
             set_error("snake_dqn_forward: occupancy query failed");
             return SNAKE_E_LAUNCH;
         }
-        g_conv_grid[vi][ci] = per_cu * cus;
+        grid = per_cu * cus;
     }
-    const unsigned gconv = (unsigned)std::min<int64_t>(batch, g_conv_grid[vi][ci]);
-    hipLaunchKernelGGL(kc, dim3(gconv), dim3(128), 0, s, ca);
+    const unsigned gconv = (unsigned)std::min<int64_t>(batch, grid);
+    hipLaunchKernelGGL(kc, dim3(gconv), dim3(64 * nw), 0, s, ca);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) { set_error("k_dqn_conv launch failed: %s", hipGetErrorString(err)); return SNAKE_E_LAUNCH; }
     FcArgs fa;

@@ -15,7 +15,7 @@ SNAKE_ABI_VERSION = 7
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
            'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version',
-           'snake_dqn_plan', 'snake_dqn_forward')
+           'snake_dqn_plan', 'snake_dqn_rows', 'snake_dqn_forward')
 
 
 class SnakeCfg(ctypes.Structure):
@@ -100,6 +100,8 @@ def lib(path=None):
                              ctypes.POINTER(SnakeOut), P]
     L.snake_render_rgb.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P, P, P]
     L.snake_dqn_plan.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(DqnLayout)]
+    L.snake_dqn_rows.argtypes = [ctypes.POINTER(DqnCfg), P, I64]
+    L.snake_dqn_rows.restype = I64
     L.snake_dqn_forward.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(DqnNet), P, I64, P, P, P, P]
     L.snake_timing_enable.argtypes = [ctypes.c_int]
     L.snake_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),

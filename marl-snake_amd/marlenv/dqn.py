@@ -67,13 +67,18 @@ class DQNForward:
         if tuple(fc1.shape) != (256, 64 * P):
             raise ValueError('fc1.weight shape %s != (256, %d)' % (tuple(fc1.shape), 64 * P))
         # k in conv3's fragment order (snake_env.h snake_dqn_layout.fc1_w) -> the
-        # reference's NCHW flatten index channel * h*w + y*w + x
+        # reference's NCHW flatten index channel * h*w + position
+        rows = (ctypes.c_int32 * P16)()
+        n = L.snake_dqn_rows(ctypes.byref(self.cfg), ctypes.cast(rows, ctypes.c_void_p), P16)
+        if n != P16:
+            check(int(n) if n < 0 else -1, L)
+        rowpos = torch.tensor(list(rows), dtype=torch.int64, device=d)
         k = torch.arange(64 * P16, device=d)
         r, j, c16, quad = k % 4, (k // 4) % 2, (k // 8) % 16, (k // 128) % 4
         half, m = (k // 512) % 2, k // 1024
-        ch, p = (2 * half + j) * 16 + c16, m * 16 + 4 * quad + r
-        src = torch.where(p < P, ch * P + p, 0)
-        fc1p = torch.where((p < P)[None, :], fc1[:, src], torch.zeros((), **f32))
+        ch, p = (2 * half + j) * 16 + c16, rowpos[m * 16 + 4 * quad + r]
+        src = torch.where(p >= 0, ch * P + p, 0)
+        fc1p = torch.where((p >= 0)[None, :], fc1[:, src], torch.zeros((), **f32))
         fc3 = g('fc3.weight')
         if tuple(fc3.shape) != (A, 128):
             raise ValueError('fc3.weight shape %s != (%d, 128)' % (tuple(fc3.shape), A))

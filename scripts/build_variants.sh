@@ -22,7 +22,8 @@ for spec in "$@"; do
         tag=${spec%%:*}; extra=${spec#*:}; dir=$ROOT/marl-snake_amd/csrc
         [[ $extra == "$spec" ]] && extra=""
     fi
-    /opt/rocm/bin/hipcc $FLAGS $extra -shared -o "$OUT/libsnake_$tag.so" "$dir/snake_kernels.hip" "$dir/snake_capi.cpp" &
+    dqn=""; [[ -f $dir/dqn_kernels.hip ]] && dqn=$dir/dqn_kernels.hip
+    /opt/rocm/bin/hipcc $FLAGS $extra -shared -o "$OUT/libsnake_$tag.so" "$dir/snake_kernels.hip" "$dir/snake_capi.cpp" $dqn &
 done
 wait
 ls -la "$OUT"/*.so

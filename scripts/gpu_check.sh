@@ -63,7 +63,7 @@ for s in "$@"; do
              step pmcSQ 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcSQ -o pmc -- $B ;;
         dqn) step dqn 300 python scripts/dqn_bench.py ;;
         dqnprof) step dqnprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dqnprof -o run --output-format csv -- python3 scripts/dqn_bench.py --no-torch ;;
-        dqnpmc) step dqnpmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES --kernel-include-regex k_dqn --output-format csv -d gpurun_out/dqnpmc -o pmc -- python3 scripts/dqn_bench.py --no-torch --steps 3 --warmup 1 ;;
+        dqnpmc) step dqnpmc 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --kernel-include-regex k_dqn --output-format csv -d gpurun_out/dqnpmc -o pmc -- python3 scripts/dqn_bench.py --no-torch --steps 3 --warmup 1 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

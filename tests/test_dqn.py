@@ -53,6 +53,17 @@ def test_dqn_plan_sizes():
     assert lay.fc1_w == 256 * 64 * 128 and lay.act_per_obs == 64 * 128
     bad = _native.DqnCfg(20, 20, 8, 3)           # full 20x20 map: vision_range <= 5 only
     assert _native.lib().snake_dqn_plan(ctypes.byref(bad), ctypes.byref(lay)) == -1
+    for vr in range(1, 6):      # GEMM rows cover every position once; a tile's border cells differ mod 16
+        W = 2 * vr + 1
+        c = _native.DqnCfg(W, W, 8, 3)
+        n = _native.lib().snake_dqn_rows(ctypes.byref(c), None, 0)
+        rows = (ctypes.c_int32 * n)()
+        assert _native.lib().snake_dqn_rows(ctypes.byref(c), ctypes.cast(rows, ctypes.c_void_p), n) == n
+        rows = list(rows)
+        assert sorted(x for x in rows if x >= 0) == list(range(W * W))
+        for t in range(n // 16):
+            q = [((p // W + 1) * (W + 2) + p % W + 1) % 16 for p in rows[16 * t:16 * t + 16] if p >= 0]
+            assert len(set(q)) == len(q)
     for h, w, c, a in ((11, 9, 8, 3), (11, 11, 12, 3), (11, 11, 40, 3), (11, 11, 8, 5), (4, 4, 8, 3)):
         assert _native.lib().snake_dqn_plan(ctypes.byref(_native.DqnCfg(h, w, c, a)), ctypes.byref(lay)) == -1
 
