@@ -172,16 +172,19 @@ __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int 
     // B one k step ahead; A (the MT fragments of a k step) one k step ahead when
     // ABUF == 2 (one wave per SIMD: nothing else hides the LDS latency)
     constexpr int ABUF = NTW >= 4 ? 2 : 1;
-    bf16x8 bcur[NTW], bnxt[NTW];
+    // B fragments PF k steps ahead (2 and 3 measured no faster)
+    constexpr int PF = 1, NR = PF + 1;
+    bf16x8 bring[NR][NTW];
     bf16x8 abuf[ABUF][G::MT];
-    load_b(bcur, 0);
+#pragma unroll
+    for (int i = 0; i < PF && i < KS; i++) load_b(bring[i], i);
     if constexpr (ABUF == 2) {
 #pragma unroll
         for (int m = 0; m < G::MT; m++) abuf[0][m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(0));
     }
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
-        if (ks + 1 < KS) load_b(bnxt, ks + 1);
+        if (ks + PF < KS) load_b(bring[(ks + PF) % NR], ks + PF);
         bf16x8 *av = abuf[ABUF == 2 ? (ks & 1) : 0];
         if constexpr (ABUF == 2) {
             if (ks + 1 < KS) {
@@ -193,14 +196,11 @@ __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int 
 #pragma unroll
             for (int m = 0; m < G::MT; m++) av[m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(ks));
         }
+        const bf16x8 *bcur = bring[ks % NR];
 #pragma unroll
         for (int m = 0; m < G::MT; m++) {
 #pragma unroll
             for (int j = 0; j < NTW; j++) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], bcur[j], acc[m][j], 0, 0, 0);
-        }
-        if (ks + 1 < KS) {
-#pragma unroll
-            for (int j = 0; j < NTW; j++) bcur[j] = bnxt[j];
         }
     }
 }
@@ -315,9 +315,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
 #pragma unroll
         for (int i = 0; i < NC; i++)
             if (cdst[i] >= 0) *reinterpret_cast<u32x4 *>(lds + cdst[i]) = bytes_to_bf16(xin[i]);
-#ifndef DQN_EXPT_NO_XIN
         if (b + gridDim.x < a.B) load_obs(b + gridDim.x);
-#endif
         conv_sync<NW>();
         {   // conv1: CP -> 32
             f32x4 acc[G::MT][NT1];
