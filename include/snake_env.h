@@ -183,9 +183,11 @@ typedef struct {
 } snake_dqn_cfg;
 
 typedef struct {        /* sizes for snake_dqn_forward (element counts) */
-    int64_t conv1_w;    /* bf16 [32][k1]: k = tap*cpad + channel, tap = ky*3 + kx, zero padded */
-    int64_t conv2_w;    /* bf16 [64][288]: k = tap*32 + channel */
-    int64_t conv3_w;    /* bf16 [64][576]: k = tap*64 + channel */
+    int64_t conv1_w;    /* bf16 B[32][k1]: k = tap*cpad + channel, tap = ky*3 + kx, zero padded */
+    int64_t conv2_w;    /* bf16 B[64][288]: k = tap*32 + channel */
+    int64_t conv3_w;    /* bf16 B[64][576]: k = tap*64 + channel; all three stored in MFMA
+                         * fragment order: element (o, k) at
+                         * ((o/16 * K/32 + k/32) * 4 + (k%32)/8) * 128 + (o%16) * 8 + k%8 */
     int64_t fc1_w;      /* bf16 [256][64*p16], k in conv3's MFMA fragment order:
                          * k = m*1024 + half*512 + quad*128 + c16*8 + j*4 + r holds
                          * channel (2*half + j)*16 + c16 at GEMM row i = m*16 + 4*quad + r,

@@ -142,27 +142,27 @@ __device__ __forceinline__ u32x4 bytes_to_bf16(uint2 v)
 // plus the lane's chunk (quad) plane. Tap offsets per k step: compile-time for
 // CIN >= 32 (one tap per k step), else the lane's precomputed toff[ks] (conv1
 // with CIN < 32: chunk included, the quad plane taken back out).
-template <int VR, int CL, int CIN, int KS, int NTW, int COUT>
+template <int VR, int CL, int CIN, int KS, int NTW, int COUT, int MTW>
 __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int *gpos, const int *toff,
                                          const uint16_t *__restrict__ wt, int nt0, int lane,
-                                         f32x4 (&acc)[Geo<VR, CL>::MT][NTW])
+                                         f32x4 (&acc)[MTW][NTW])
 {
     using G = Geo<VR, CL>;
-    const int r16 = lane & 15, kq = 8 * (lane >> 4);
     constexpr int K = KS * 32;
-    // weights through a buffer descriptor: the lane's offset in one VGPR, the
-    // (tile, k step) part a scalar offset -- no per-load 64-bit addresses
+    // weights in fragment order (1 KB per (channel tile, k step), lane-major:
+    // every load is 1 KB contiguous) through a buffer descriptor: the lane's
+    // offset in one VGPR, the (tile, k step) part a scalar offset
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(wt), 0, 2 * K * COUT, 0x00020000);
-    const int voff = 2 * ((nt0 * 16 + r16) * K + kq);
+    const int voff = 16 * lane;
     auto load_b = [&](bf16x8 (&bw)[NTW], int ks) {
 #pragma unroll
         for (int j = 0; j < NTW; j++) {
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (j * 16 * K + ks * 32), 0);
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 1024 * ((nt0 + j) * KS + ks), 0);
             bw[j] = __builtin_bit_cast(bf16x8, v);
         }
     };
 #pragma unroll
-    for (int m = 0; m < G::MT; m++)
+    for (int m = 0; m < MTW; m++)
 #pragma unroll
         for (int j = 0; j < NTW; j++) acc[m][j] = (f32x4)0.0f;
     auto a_off = [&](int ks) {
@@ -175,12 +175,12 @@ __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int 
     // B fragments PF k steps ahead (2 and 3 measured no faster)
     constexpr int PF = 1, NR = PF + 1;
     bf16x8 bring[NR][NTW];
-    bf16x8 abuf[ABUF][G::MT];
+    bf16x8 abuf[ABUF][MTW];
 #pragma unroll
     for (int i = 0; i < PF && i < KS; i++) load_b(bring[i], i);
     if constexpr (ABUF == 2) {
 #pragma unroll
-        for (int m = 0; m < G::MT; m++) abuf[0][m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(0));
+        for (int m = 0; m < MTW; m++) abuf[0][m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(0));
     }
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
@@ -189,16 +189,16 @@ __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int 
         if constexpr (ABUF == 2) {
             if (ks + 1 < KS) {
 #pragma unroll
-                for (int m = 0; m < G::MT; m++)
+                for (int m = 0; m < MTW; m++)
                     abuf[(ks + 1) & 1][m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(ks + 1));
             }
         } else {
 #pragma unroll
-            for (int m = 0; m < G::MT; m++) av[m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(ks));
+            for (int m = 0; m < MTW; m++) av[m] = *reinterpret_cast<const bf16x8 *>(lds + src + gpos[m] + a_off(ks));
         }
         const bf16x8 *bcur = bring[ks % NR];
 #pragma unroll
-        for (int m = 0; m < G::MT; m++) {
+        for (int m = 0; m < MTW; m++) {
 #pragma unroll
             for (int j = 0; j < NTW; j++) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], bcur[j], acc[m][j], 0, 0, 0);
         }
@@ -206,9 +206,9 @@ __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int 
 }
 
 // bias + ReLU -> bf16 into the interior of a chunk-major border image
-template <int VR, int CL, int NTW>
+template <int VR, int CL, int NTW, int MTW>
 __device__ __forceinline__ void conv_store_lds(uint8_t *lds, int dst, const uint16_t *ptab, int nt0, int lane,
-                                               const float (&bias)[NTW], f32x4 (&acc)[Geo<VR, CL>::MT][NTW])
+                                               const float (&bias)[NTW], f32x4 (&acc)[MTW][NTW])
 {
     using G = Geo<VR, CL>;
     const int r16 = lane & 15, quad = lane >> 4;
@@ -218,7 +218,7 @@ __device__ __forceinline__ void conv_store_lds(uint8_t *lds, int dst, const uint
         const float bb = bias[j];
         const int cbase = dst + (co >> 3) * G::CH + 2 * (co & 7);
 #pragma unroll
-        for (int m = 0; m < G::MT; m++) {
+        for (int m = 0; m < MTW; m++) {
             const uint2 pq = *reinterpret_cast<const uint2 *>(ptab + m * 16 + 4 * quad);
             const uint32_t q[4] = {pq.x & 0xffffu, pq.x >> 16, pq.y & 0xffffu, pq.y >> 16};
 #pragma unroll
@@ -249,16 +249,22 @@ __device__ __forceinline__ void conv_sync()
 
 // NW waves per observation (1: no workgroup barriers, all four channel tiles of
 // conv2/conv3 per wave, each A fragment feeding four MFMAs; 2: two waves split
-// the channel tiles).
+// the channel tiles; 4: two channel halves x two row halves, for twice the
+// waves per SIMD at the same LDS, each weight fragment loaded by two waves).
+// ptab is passed to the epilogue offset to the wave's first row tile.
 template <int VR, int CL, int NW>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 1 ? 1 : 2))) k_dqn_conv(const ConvArgs a)
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW))) k_dqn_conv(const ConvArgs a)
 {
     using G = Geo<VR, CL>;
     constexpr int NT = 64 * NW;
+    constexpr int MH = NW == 4 ? 2 : 1, NH = NW == 1 ? 1 : 2;   // row-tile halves x channel halves
+    constexpr int MTW = G::MT / MH;
+    static_assert(G::MT % MH == 0, "row halves need an even tile count");
     constexpr int NC = (G::NCELL0 + NT - 1) / NT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int w = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform
+    const int wv = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform
+    const int w = NH == 1 ? 0 : (wv & 1), m0 = MH == 1 ? 0 : (wv >> 1) * MTW;   // channel half, first row tile
     const int r16 = lane & 15;
     uint16_t *ptab = reinterpret_cast<uint16_t *>(lds + G::OFFT);
     for (int i = tid; i < G::P16; i += NT) ptab[i] = (uint16_t)0xffffu;
@@ -267,10 +273,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
     for (int p = tid; p < G::P; p += NT) ptab[dqn_row_of(p, G::W)] = (uint16_t)dqn_bidx(p, G::W);
     conv_sync<NW>();
     const int qplane = (lane >> 4) * G::CH;
-    int gpos[G::MT];
+    int gpos[MTW];
 #pragma unroll
-    for (int m = 0; m < G::MT; m++) {
-        const int q = ptab[m * 16 + r16];
+    for (int m = 0; m < MTW; m++) {
+        const int q = ptab[(m0 + m) * 16 + r16];
         gpos[m] = ((q != 0xffff ? q : G::padq(r16)) - G::BW - 1) * 16 + qplane;
     }
     // conv1 per-lane tap offsets (k = tap * CP + channel; taps past the 9th meet zero weights)
@@ -298,7 +304,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
 #pragma unroll
         for (int i = 0; i < NC; i++) xin[i] = csrc[i] >= 0 ? *reinterpret_cast<const uint2 *>(x + csrc[i]) : make_uint2(0, 0);
     };
-    constexpr int NT1 = 2 / NW, NT3 = 4 / NW;
+    constexpr int NT1 = 2 / NH, NT3 = 4 / NH;
     // biases of this lane's output channels, loaded once
     float bias1[NT1], bias2[NT3], bias3[NT3];
 #pragma unroll
@@ -318,9 +324,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
         if (b + gridDim.x < a.B) load_obs(b + gridDim.x);
         conv_sync<NW>();
         {   // conv1: CP -> 32
-            f32x4 acc[G::MT][NT1];
+            f32x4 acc[MTW][NT1];
             conv_mma<VR, CL, G::CP, G::K1S, NT1, 32>(lds, G::OFF2, gpos, toff1, a.w1, w * NT1, lane, acc);
-            conv_store_lds<VR, CL, NT1>(lds, G::OFF1, ptab, w * NT1, lane, bias1, acc);
+            conv_store_lds<VR, CL, NT1>(lds, G::OFF1, ptab + m0 * 16, w * NT1, lane, bias1, acc);
         }
         conv_sync<NW>();
         // the input image is dead: restore a2's zero border
@@ -333,14 +339,14 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
             *reinterpret_cast<u32x4 *>(lds + G::OFF2 + chunk * G::CH + q * 16) = (u32x4)0u;
         }
         {   // conv2: 32 -> 64
-            f32x4 acc[G::MT][NT3];
+            f32x4 acc[MTW][NT3];
             conv_mma<VR, CL, 32, 9, NT3, 64>(lds, G::OFF1, gpos, nullptr, a.w2, w * NT3, lane, acc);
-            conv_store_lds<VR, CL, NT3>(lds, G::OFF2, ptab, w * NT3, lane, bias2, acc);
+            conv_store_lds<VR, CL, NT3>(lds, G::OFF2, ptab + m0 * 16, w * NT3, lane, bias2, acc);
         }
         conv_sync<NW>();
         {   // conv3: 64 -> 64 -> global, in MFMA fragment order
             // (k = m*1024 + half*512 + lane*8 + j*4 + r, channel tile 2*half + j)
-            f32x4 acc[G::MT][NT3];
+            f32x4 acc[MTW][NT3];
             conv_mma<VR, CL, 64, 18, NT3, 64>(lds, G::OFF2, gpos, nullptr, a.w3, w * NT3, lane, acc);
             u32x4 *dst = reinterpret_cast<u32x4 *>(a.act + b * (int64_t)(64 * G::P16)) + lane;
 #pragma unroll
@@ -348,13 +354,13 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
                 const int half = w * (NT3 / 2) + h;
                 const float b0 = bias3[2 * h], b1 = bias3[2 * h + 1];
 #pragma unroll
-                for (int m = 0; m < G::MT; m++) {
+                for (int m = 0; m < MTW; m++) {
                     u32x4 v;
                     v[0] = pack2(fmaxf(acc[m][2 * h][0] + b0, 0.0f), fmaxf(acc[m][2 * h][1] + b0, 0.0f));
                     v[1] = pack2(fmaxf(acc[m][2 * h][2] + b0, 0.0f), fmaxf(acc[m][2 * h][3] + b0, 0.0f));
                     v[2] = pack2(fmaxf(acc[m][2 * h + 1][0] + b1, 0.0f), fmaxf(acc[m][2 * h + 1][1] + b1, 0.0f));
                     v[3] = pack2(fmaxf(acc[m][2 * h + 1][2] + b1, 0.0f), fmaxf(acc[m][2 * h + 1][3] + b1, 0.0f));
-                    dst[m * 128 + half * 64] = v;
+                    dst[(m0 + m) * 128 + half * 64] = v;
                 }
             }
         }
@@ -549,27 +555,39 @@ using namespace snake::dqn;
 
 namespace {
 typedef void (*conv_kernel_t)(ConvArgs);
+struct ConvKernel {
+    conv_kernel_t k;
+    int nw;   // waves per observation (= workgroup size / 64)
+};
+template <int VR, int CL, int NW>
+constexpr ConvKernel conv_kernel()
+{
+    if constexpr (NW == 4 && Geo<VR, CL>::MT % 2 != 0) return {k_dqn_conv<VR, CL, 2>, 2};   // odd tile count
+    else return {k_dqn_conv<VR, CL, NW>, NW};
+}
 template <int NW>
 struct ConvTable {
-    conv_kernel_t k[5][3] = {
-        {k_dqn_conv<1, 3, NW>, k_dqn_conv<1, 4, NW>, k_dqn_conv<1, 5, NW>},
-        {k_dqn_conv<2, 3, NW>, k_dqn_conv<2, 4, NW>, k_dqn_conv<2, 5, NW>},
-        {k_dqn_conv<3, 3, NW>, k_dqn_conv<3, 4, NW>, k_dqn_conv<3, 5, NW>},
-        {k_dqn_conv<4, 3, NW>, k_dqn_conv<4, 4, NW>, k_dqn_conv<4, 5, NW>},
-        {k_dqn_conv<5, 3, NW>, k_dqn_conv<5, 4, NW>, k_dqn_conv<5, 5, NW>},
+    ConvKernel k[5][3] = {
+        {conv_kernel<1, 3, NW>(), conv_kernel<1, 4, NW>(), conv_kernel<1, 5, NW>()},
+        {conv_kernel<2, 3, NW>(), conv_kernel<2, 4, NW>(), conv_kernel<2, 5, NW>()},
+        {conv_kernel<3, 3, NW>(), conv_kernel<3, 4, NW>(), conv_kernel<3, 5, NW>()},
+        {conv_kernel<4, 3, NW>(), conv_kernel<4, 4, NW>(), conv_kernel<4, 5, NW>()},
+        {conv_kernel<5, 3, NW>(), conv_kernel<5, 4, NW>(), conv_kernel<5, 5, NW>()},
     };
 };
 const ConvTable<1> kConv1;
 const ConvTable<2> kConv2;
-int g_conv_grid[2][5][3];
-// waves per observation in k_dqn_conv: SNAKE_DQN_WAVES=1|2 (default 2; one wave
+const ConvTable<4> kConv4;
+int g_conv_grid[3][5][3];
+// waves per observation in k_dqn_conv: SNAKE_DQN_WAVES=1|2|4 (default 2; one wave
 // per observation measured 35 % slower: nothing hides its LDS / L2 latencies)
 int conv_waves()
 {
     static int nw = 0;
     if (!nw) {
         const char *e = getenv("SNAKE_DQN_WAVES");
-        nw = (e && atoi(e) == 1) ? 1 : 2;
+        const int v = e ? atoi(e) : 0;
+        nw = (v == 1 || v == 4) ? v : 2;
     }
     return nw;
 }
@@ -640,9 +658,11 @@ extern "C" int snake_dqn_forward(const snake_dqn_cfg *cfg, const snake_dqn_net *
     ca.b1 = net->conv1_b; ca.b2 = net->conv2_b; ca.b3 = net->conv3_b;
     ca.act = act_scratch;
     const int vi = (cfg->height - 3) / 2, ci = lay.cpad == 8 ? 0 : (lay.cpad == 16 ? 1 : 2);
-    const int nw = conv_waves();
-    const conv_kernel_t kc = nw == 1 ? kConv1.k[vi][ci] : kConv2.k[vi][ci];
-    int &grid = g_conv_grid[nw - 1][vi][ci];
+    const int want = conv_waves();
+    const ConvKernel ck = want == 1 ? kConv1.k[vi][ci] : (want == 4 ? kConv4.k[vi][ci] : kConv2.k[vi][ci]);
+    const conv_kernel_t kc = ck.k;
+    const int nw = ck.nw;
+    int &grid = g_conv_grid[want == 1 ? 0 : (want == 2 ? 1 : 2)][vi][ci];
     if (!grid) {   // persistent grid: the resident workgroups of the whole device
         int per_cu = 0, dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||

@@ -52,13 +52,15 @@ class DQNForward:
             return t.to(torch.bfloat16).contiguous().view(torch.int16)
 
         def conv_pack(w, cin_pad, k_pad):
-            # [out][in][ky][kx] -> [out][k = (ky*3 + kx) * cin_pad + ci], zero padded
+            # [out][in][ky][kx] -> B[out][k = (ky*3 + kx) * cin_pad + ci], zero padded,
+            # stored in MFMA fragment order: [out/16][k/32][k%32 / 8][out%16][8]
             out_ch, cin = w.shape[0], w.shape[1]
             t = torch.zeros((out_ch, 9, cin_pad), **f32)
             t[:, :, :cin] = w.permute(0, 2, 3, 1).reshape(out_ch, 9, cin)
             flat = torch.zeros((out_ch, k_pad), **f32)
             flat[:, :9 * cin_pad] = t.reshape(out_ch, 9 * cin_pad)
-            return bits(flat)
+            frag = flat.reshape(out_ch // 16, 16, k_pad // 32, 4, 8).permute(0, 2, 3, 1, 4)
+            return bits(frag.contiguous().reshape(out_ch, k_pad))
 
         w1, w2, w3 = g('conv1.weight'), g('conv2.weight'), g('conv3.weight')
         if tuple(w1.shape) != (32, C, 3, 3) or tuple(w2.shape) != (64, 32, 3, 3) or tuple(w3.shape) != (64, 64, 3, 3):
