@@ -404,49 +404,45 @@ __global__ void __launch_bounds__(512) k_dqn_fc(const FcArgs a)
     const int r16 = lane & 15, quad = lane >> 4, kq = 8 * quad;
     const int64_t row0 = (int64_t)blockIdx.x * kFcObs + wv * kFcRowsPerWave;
     // A rows of this lane (row tiles 0 and 1); rows past B read row 0 (results unused)
-    const uint16_t *arow[2];
-#pragma unroll
-    for (int m = 0; m < 2; m++) {
-        const int64_t r = row0 + m * 16 + r16;
-        arow[m] = a.act + (r < a.B ? r : 0) * (int64_t)a.K + kq;
-    }
-    // weight staging: slot = tid + 512 i -> row n = slot / 8, 16-byte chunk c8 = slot % 8 of the stage
-    const uint16_t *wsrc[4];
-    int wdst[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int slot = tid + 512 * i, n = slot >> 3, c8 = slot & 7;
-        wsrc[i] = a.w4 + (int64_t)n * a.K + c8 * 8;
-        wdst[i] = fc_tile_off(c8 >> 2, n, c8 & 3);
-    }
+    // buffer descriptors: 32-bit lane offsets, the (row tile, stage, chunk) parts
+    // as scalar offsets; the activation descriptor ends at the last valid row,
+    // so rows past B read zeros
+    const int64_t wg_row0 = (int64_t)blockIdx.x * kFcObs;
+    const int64_t rows_here = a.B - wg_row0 < kFcObs ? a.B - wg_row0 : kFcObs;
+    const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(a.act + wg_row0 * a.K), 0,
+                                                       (int)(rows_here * a.K * 2), 0x00020000);
+    const auto rs_w = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(a.w4), 0, 256 * a.K * 2, 0x00020000);
+    const int va = ((wv * kFcRowsPerWave + r16) * a.K + kq) * 2;
+    // weight staging: slot = tid + 512 i -> row n = tid / 8 + 64 i, 16-byte chunk tid % 8 of the stage
+    const int vw = ((tid >> 3) * a.K + (tid & 7) * 8) * 2;
+    const int wdst = fc_tile_off((tid & 7) >> 2, tid >> 3, tid & 3);
     const int nstage = a.K / 64;
     u32x4 rb[4];
-    bf16x8 ra[2][2], an[2][2];
+    bf16x8 a0[2][2], a1[2][2];   // A of even / odd stages (no register copies between stages)
     auto load_b = [&](int st) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) rb[i] = *reinterpret_cast<const u32x4 *>(wsrc[i] + st * 64);
+        for (int i = 0; i < 4; i++) rb[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_w, vw, i * 64 * a.K * 2 + st * 128, 0);
     };
     auto load_a = [&](int st, bf16x8 (&dst)[2][2]) {
 #pragma unroll
         for (int m = 0; m < 2; m++)
 #pragma unroll
-            for (int h = 0; h < 2; h++) dst[m][h] = *reinterpret_cast<const bf16x8 *>(arow[m] + st * 64 + h * 32);
+            for (int h = 0; h < 2; h++)
+                dst[m][h] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                           rs_a, va, m * 16 * a.K * 2 + st * 128 + h * 64, 0));
     };
     auto store_b = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) *reinterpret_cast<u32x4 *>(&bt[buf][wdst[i]]) = rb[i];
+        for (int i = 0; i < 4; i++) *reinterpret_cast<u32x4 *>(&bt[buf][wdst + 4096 * i]) = rb[i];
     };
     f32x4 acc[2][16];
 #pragma unroll
     for (int m = 0; m < 2; m++)
 #pragma unroll
         for (int n = 0; n < 16; n++) acc[m][n] = (f32x4)0.0f;
-    load_b(0);
-    load_a(0, ra);
-    store_b(0);
-    if (nstage > 1) { load_b(1); load_a(1, an); }
-    __syncthreads();
-    for (int st = 0; st < nstage; st++) {
+    // stage st: MFMAs on A(st) (in ra) and the LDS tile st & 1; then the tile
+    // st + 1 (loaded a stage ago) goes to LDS and A / B of stage st + 2 are issued
+    auto stage = [&](int st, bf16x8 (&ra)[2][2]) {
         const int buf = st & 1;
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -457,16 +453,25 @@ __global__ void __launch_bounds__(512) k_dqn_fc(const FcArgs a)
                 acc[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[1][h], bv, acc[1][n], 0, 0, 0);
             }
         }
-        if (st + 1 < nstage) {
-            store_b(buf ^ 1);
-#pragma unroll
-            for (int m = 0; m < 2; m++)
-#pragma unroll
-                for (int h = 0; h < 2; h++) ra[m][h] = an[m][h];
-            if (st + 2 < nstage) { load_b(st + 2); load_a(st + 2, an); }
-        }
+        // unconditional (clamped) so the wait counts are the same on every path
+        store_b(buf ^ 1);
+        const int nx = st + 2 < nstage ? st + 2 : nstage - 1;
+        load_b(nx);
+        load_a(nx, ra);
         __syncthreads();
+    };
+    load_b(0);
+    load_a(0, a0);
+    store_b(0);
+    load_b(nstage > 1 ? 1 : 0);
+    load_a(nstage > 1 ? 1 : 0, a1);
+    __syncthreads();
+    int st = 0;
+    for (; st + 1 < nstage; st += 2) {
+        stage(st, a0);
+        stage(st + 1, a1);
     }
+    if (st < nstage) stage(st, a0);
     // fc2 and fc3: waves 0-3, then 4-7, each with a 16 KB slice of the tile buffers
     // (every wave passes one barrier: after its epilogue, or before it)
     if (wv >= 4) __syncthreads();
