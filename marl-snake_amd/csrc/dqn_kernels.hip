@@ -169,9 +169,8 @@ __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int 
         if constexpr (CIN >= 32) return G::tapoff((ks * 32) / CIN) + ((ks * 32) % CIN) / 8 * G::CH;
         else return toff[ks];
     };
-    // B one k step ahead; A (the MT fragments of a k step) one k step ahead when
-    // ABUF == 2 (one wave per SIMD: nothing else hides the LDS latency)
-    constexpr int ABUF = NTW >= 4 ? 2 : 1;
+    // B and A (the row tiles' fragments of a k step) one k step ahead
+    constexpr int ABUF = 2;
     // B fragments PF k steps ahead (2 and 3 measured no faster)
     constexpr int PF = 1, NR = PF + 1;
     bf16x8 bring[NR][NTW];
@@ -185,6 +184,9 @@ __device__ __forceinline__ void conv_mma(const uint8_t *lds, int src, const int 
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
         if (ks + PF < KS) load_b(bring[(ks + PF) % NR], ks + PF);
+        // keep the prefetch ahead of this k step's MFMAs (the scheduler otherwise
+        // sinks it next to its use: 4.78 -> 4.61 ms with the pin at 4 waves)
+        __builtin_amdgcn_sched_barrier(0);
         bf16x8 *av = abuf[ABUF == 2 ? (ks & 1) : 0];
         if constexpr (ABUF == 2) {
             if (ks + 1 < KS) {
@@ -584,15 +586,16 @@ const ConvTable<1> kConv1;
 const ConvTable<2> kConv2;
 const ConvTable<4> kConv4;
 int g_conv_grid[3][5][3];
-// waves per observation in k_dqn_conv: SNAKE_DQN_WAVES=1|2|4 (default 2; one wave
-// per observation measured 35 % slower: nothing hides its LDS / L2 latencies)
+// waves per observation in k_dqn_conv: SNAKE_DQN_WAVES=1|2|4 (default 4, two
+// for odd row-tile counts; forward at 262144 observations: 4.51 / 4.57 / 5.91 ms
+// for 4 / 2 / 1)
 int conv_waves()
 {
     static int nw = 0;
     if (!nw) {
         const char *e = getenv("SNAKE_DQN_WAVES");
         const int v = e ? atoi(e) : 0;
-        nw = (v == 1 || v == 4) ? v : 2;
+        nw = (v == 1 || v == 2) ? v : 4;
     }
     return nw;
 }
