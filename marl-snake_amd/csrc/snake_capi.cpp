@@ -290,6 +290,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     const int slots = ev_slots ? std::max(1, std::min(kResetSlots, atoi(ev_slots))) : kResetSlots;
     k->reset_slots = (int)std::min<int64_t>(N, slots);
     k->spawn_prio = ev_prio ? std::max(0, std::min(3, atoi(ev_prio))) : 1;
+    // k_encode above the spawn-ahead jobs: the bandwidth-bound encodes then keep
+    // HBM busy while the compute-bound workers fill the issue gaps (SNAKE_ENCODE_PRIO,
+    // default 2: step 0.1275 -> 0.1200 ms at cfg3; 0 = hardware default)
+    static const char *ev_eprio = getenv("SNAKE_ENCODE_PRIO");
+    k->encode_prio = ev_eprio ? std::max(0, std::min(3, atoi(ev_eprio))) : 2;
     k->q_envs_per_block = kWave / (k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16));
     {
         const int64_t blocks = (N + k->q_envs_per_block - 1) / k->q_envs_per_block;

@@ -55,6 +55,7 @@ struct KCfg {
     int q_cap;                  // queue entries per shard
     int spawn_thr;              // queue spawn-ahead when <= this many snakes live (-1: off)
     int spawn_prio;             // wave priority of the spawn-ahead jobs (resets: 3)
+    int encode_prio;            // wave priority of k_encode (beside the reset workers)
     int diag;                   // count spawn-ahead hits/jobs (while timing is enabled)
     double rf, rk, rl, rw, rt, max_steps;
 };

@@ -1326,6 +1326,9 @@ __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state s
     const bool prof_ = (e & 511) == 0 && (e >> 9) < 128;
     if (prof_) OBSPROF(256 + (e >> 9), lane);
     if (c.autoreset && o.ep_done[e]) return;          // its reset writes the obs
+    if (c.encode_prio == 1) __builtin_amdgcn_s_setprio(1);      // (setprio takes an immediate)
+    else if (c.encode_prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (c.encode_prio == 3) __builtin_amdgcn_s_setprio(3);
     const int fs = c.fs, S = c.S;
     uint8_t *frames = lds + c.lds_frames;
     int *org = reinterpret_cast<int *>(lds + c.lds_centers);
