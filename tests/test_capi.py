@@ -60,7 +60,7 @@ def test_plan_sizes(native):
     c = cfg(native, height=44, width=44, num_snakes=4)
     lay2 = native.SnakeLayout()
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay2)) == 0
-    assert lay2.n_cand == 20168 and lay2.jscratch == 2048 * (20168 + 64) * 4   # global link tables
+    assert lay2.n_cand == 20168 and lay2.jscratch == 2560 * (20168 + 64) * 4   # global link tables
     assert lay.grid == 8192 * 4 * 1600
 
 
