@@ -8,6 +8,7 @@ next kernel's start (same step order), over the last --last launches.
 import argparse
 import collections
 import csv
+import json
 import statistics
 
 
@@ -28,9 +29,9 @@ def main():
             gap[f'{n}->{ev[i + 1][0]}'].append(ev[i + 1][1] - e)
     starts = [s for n, s, e in ev if n == 'k_logic']
     per_step = statistics.median([b - a for a, b in zip(starts, starts[1:])]) if len(starts) > 1 else None
-    print({'step_us': per_step,
-           'dur_us': {k: round(statistics.median(v), 1) for k, v in dur.items()},
-           'gap_us': {k: round(statistics.median(v), 1) for k, v in gap.items()}})
+    print(json.dumps({'step_us': round(per_step, 2) if per_step is not None else None,
+                      'dur_us': {k: round(statistics.median(v), 1) for k, v in dur.items()},
+                      'gap_us': {k: round(statistics.median(v), 1) for k, v in gap.items()}}))
 
 
 if __name__ == '__main__':
