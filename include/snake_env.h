@@ -180,6 +180,8 @@ int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
  * vision_range in [1, 5], c = 8*frame_stack <= 32, A <= 4. */
 typedef struct {
     int32_t height, width, channels, num_actions;
+    int32_t conv_waves;     /* waves per observation in the conv kernel: 1, 2, 4; 0 = default (4,
+                             * or 2 when the row-tile count is odd; SNAKE_DQN_WAVES overrides 0) */
 } snake_dqn_cfg;
 
 typedef struct {        /* sizes for snake_dqn_forward (element counts) */

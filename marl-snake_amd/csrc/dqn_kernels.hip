@@ -586,9 +586,9 @@ const ConvTable<1> kConv1;
 const ConvTable<2> kConv2;
 const ConvTable<4> kConv4;
 int g_conv_grid[3][5][3];
-// waves per observation in k_dqn_conv: SNAKE_DQN_WAVES=1|2|4 (default 4, two
-// for odd row-tile counts; forward at 262144 observations: 4.51 / 4.57 / 5.91 ms
-// for 4 / 2 / 1)
+// waves per observation in k_dqn_conv when snake_dqn_cfg.conv_waves is 0:
+// SNAKE_DQN_WAVES=1|2|4, else 4 (two for odd row-tile counts). Forward at 262144
+// observations: 4.51 / 4.57 / 5.91 ms for 4 / 2 / 1.
 int conv_waves()
 {
     static int nw = 0;
@@ -614,6 +614,10 @@ extern "C" int snake_dqn_plan(const snake_dqn_cfg *cfg, snake_dqn_layout *out)
         return SNAKE_E_CONFIG;
     }
     if (A < 1 || A > 4) { set_error("snake_dqn: num_actions must be in [1, 4] (got %d)", A); return SNAKE_E_CONFIG; }
+    if (cfg->conv_waves != 0 && cfg->conv_waves != 1 && cfg->conv_waves != 2 && cfg->conv_waves != 4) {
+        set_error("snake_dqn: conv_waves must be 0, 1, 2 or 4 (got %d)", cfg->conv_waves);
+        return SNAKE_E_CONFIG;
+    }
     int cl = 3;
     while ((1 << cl) < C) cl++;
     const int MT = dqn_tiles(W), P16 = MT * 16, CP = 1 << cl;
@@ -666,7 +670,7 @@ extern "C" int snake_dqn_forward(const snake_dqn_cfg *cfg, const snake_dqn_net *
     ca.b1 = net->conv1_b; ca.b2 = net->conv2_b; ca.b3 = net->conv3_b;
     ca.act = act_scratch;
     const int vi = (cfg->height - 3) / 2, ci = lay.cpad == 8 ? 0 : (lay.cpad == 16 ? 1 : 2);
-    const int want = conv_waves();
+    const int want = cfg->conv_waves ? cfg->conv_waves : conv_waves();
     const ConvKernel ck = want == 1 ? kConv1.k[vi][ci] : (want == 4 ? kConv4.k[vi][ci] : kConv2.k[vi][ci]);
     const conv_kernel_t kc = ck.k;
     const int nw = ck.nw;

@@ -50,7 +50,7 @@ class SnakeOut(ctypes.Structure):
 
 class DqnCfg(ctypes.Structure):
     _fields_ = [('height', ctypes.c_int32), ('width', ctypes.c_int32), ('channels', ctypes.c_int32),
-                ('num_actions', ctypes.c_int32)]
+                ('num_actions', ctypes.c_int32), ('conv_waves', ctypes.c_int32)]
 
 
 class DqnLayout(ctypes.Structure):

@@ -28,15 +28,16 @@ def _torch():
 class DQNForward:
     """DQN(input_shape=(N, h, w, c), num_actions) forward on uint8 NHWC observations.
 
-    state: a state dict (or nn.Module) of the reference DQN (conv1..conv3, fc1..fc3)."""
+    state: a state dict (or nn.Module) of the reference DQN (conv1..conv3, fc1..fc3).
+    conv_waves: waves per observation in the conv kernel (0 = the library default)."""
 
-    def __init__(self, state, height, width, channels, num_actions=3, device=None, lib_path=None):
+    def __init__(self, state, height, width, channels, num_actions=3, device=None, lib_path=None, conv_waves=0):
         torch = _torch()
         if hasattr(state, 'state_dict'):
             state = state.state_dict()
         self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
         self._L = L = lib(lib_path)
-        self.cfg = DqnCfg(int(height), int(width), int(channels), int(num_actions))
+        self.cfg = DqnCfg(int(height), int(width), int(channels), int(num_actions), int(conv_waves))
         lay = DqnLayout()
         check(L.snake_dqn_plan(ctypes.byref(self.cfg), ctypes.byref(lay)), L)
         self.layout = lay

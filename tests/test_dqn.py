@@ -64,8 +64,9 @@ def test_dqn_plan_sizes():
         for t in range(n // 16):
             q = [((p // W + 1) * (W + 2) + p % W + 1) % 16 for p in rows[16 * t:16 * t + 16] if p >= 0]
             assert len(set(q)) == len(q)
-    for h, w, c, a in ((11, 9, 8, 3), (11, 11, 12, 3), (11, 11, 40, 3), (11, 11, 8, 5), (4, 4, 8, 3)):
-        assert _native.lib().snake_dqn_plan(ctypes.byref(_native.DqnCfg(h, w, c, a)), ctypes.byref(lay)) == -1
+    for h, w, c, a, nw in ((11, 9, 8, 3, 0), (11, 11, 12, 3, 0), (11, 11, 40, 3, 0), (11, 11, 8, 5, 0),
+                           (4, 4, 8, 3, 0), (11, 11, 8, 3, 3)):
+        assert _native.lib().snake_dqn_plan(ctypes.byref(_native.DqnCfg(h, w, c, a, nw)), ctypes.byref(lay)) == -1
 
 
 def _obs_batch(B, vr, fs, S=4, seed=0):
@@ -81,9 +82,10 @@ def _obs_batch(B, vr, fs, S=4, seed=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('B,vr,fs', [(512, 5, 1), (333, 5, 1), (64, 4, 2), (40, 3, 4), (1, 5, 1),
-                                     (257, 2, 1), (100, 1, 3), (3000, 5, 2)])
-def test_dqn_forward_matches_fp32_reference(B, vr, fs):
+@pytest.mark.parametrize('B,vr,fs,waves', [(512, 5, 1, 0), (333, 5, 1, 0), (64, 4, 2, 0), (40, 3, 4, 0),
+                                           (1, 5, 1, 0), (257, 2, 1, 0), (100, 1, 3, 0), (3000, 5, 2, 0),
+                                           (333, 5, 1, 1), (333, 5, 1, 2), (64, 4, 2, 1), (257, 2, 1, 4)])
+def test_dqn_forward_matches_fp32_reference(B, vr, fs, waves):
     from marlenv.dqn import DQNForward
     torch.manual_seed(1)
     h = w = 2 * vr + 1
@@ -91,7 +93,7 @@ def test_dqn_forward_matches_fp32_reference(B, vr, fs):
     ref = RefDQN(h, w, c, 3).cuda()
     obs = _obs_batch(B, vr, fs)
     assert obs.shape == (B, h, w, c)
-    net = DQNForward(ref, h, w, c, 3)
+    net = DQNForward(ref, h, w, c, 3, conv_waves=waves)
     q = net(obs)
     feat = net.forward_features(obs)
     torch.cuda.synchronize()
