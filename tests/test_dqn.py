@@ -121,3 +121,25 @@ def test_dqn_rejects_non_uint8():
     net = DQNForward(ref, 11, 11, 8, 3)
     with pytest.raises(TypeError):
         net(torch.zeros((2, 11, 11, 8), device='cuda'))
+
+
+@pytest.mark.gpu
+def test_dqn_full_batch_sampled():
+    """The bench's batch (65 536 envs x 4 snakes = 262 144 observations, every
+    persistent workgroup running many observations, multi-GB scratch offsets):
+    512 sampled rows against the fp32 reference."""
+    from marlenv.dqn import DQNForward
+    torch.manual_seed(3)
+    obs = _obs_batch(262144, 5, 1, seed=5)
+    ref = RefDQN(11, 11, 8, 3).cuda()
+    net = DQNForward(ref, 11, 11, 8, 3)
+    q = net(obs)
+    torch.cuda.synchronize()
+    g = torch.Generator(device='cuda').manual_seed(7)
+    rows = torch.cat([torch.randint(0, 262144, (508,), generator=g, device='cuda'),
+                      torch.tensor([0, 1, 262142, 262143], device='cuda')])
+    with torch.no_grad():
+        q32 = ref(obs[rows])
+    scale = float(q32.abs().max())
+    assert torch.isfinite(q).all()
+    assert float((q[rows] - q32).abs().max()) <= 2e-2 * scale + 1e-3
