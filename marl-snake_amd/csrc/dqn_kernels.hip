@@ -99,8 +99,13 @@ struct Geo {
     static constexpr int CH = ((NB + 15) / 16) * 16 * 16;       // bytes per 8-channel chunk plane
     static constexpr int K1S = (9 * CP + 31) / 32;              // conv1 k steps
     static constexpr int OFF1 = 0;                              // a1: 4 planes
-    static constexpr int OFF2 = 4 * CH;                         // a2: 8 planes; a0 (CP/8 planes) overlays it
-    static constexpr int OFFT = OFF2 + 8 * CH;                  // u16 [P16]: border index of GEMM row, 0xffff pad
+    static constexpr int OFF2 = 4 * CH;                         // a2: 8 planes
+    // a0 (CP/8 planes) in its own planes when four workgroups per CU still fit
+    // (then no barrier closes an observation and a2's border is zeroed once),
+    // else over a2 (its border rewritten after conv1 of every observation)
+    static constexpr bool SEP = 4 * ((12 + CP / 8) * CH + P16 * 2) <= 160 * 1024;
+    static constexpr int OFF0 = SEP ? 12 * CH : OFF2;
+    static constexpr int OFFT = SEP ? 12 * CH + (CP / 8) * CH : 12 * CH;   // u16 [P16]: border index of GEMM row
     static constexpr int LDS = OFFT + P16 * 2;
     static constexpr int NCELL0 = NB * CP / 8;                  // 16-byte cells of the input image
     static constexpr int NBORDER = NB - P;
@@ -270,7 +275,8 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
     const int r16 = lane & 15;
     uint16_t *ptab = reinterpret_cast<uint16_t *>(lds + G::OFFT);
     for (int i = tid; i < G::P16; i += NT) ptab[i] = (uint16_t)0xffffu;
-    for (int i = tid; i < 4 * G::CH / 16; i += NT) reinterpret_cast<u32x4 *>(lds + G::OFF1)[i] = (u32x4)0u;
+    // zero a1 (and a2 when the input image has its own planes): borders stay zero
+    for (int i = tid; i < (G::SEP ? 12 : 4) * G::CH / 16; i += NT) reinterpret_cast<u32x4 *>(lds + G::OFF1)[i] = (u32x4)0u;
     conv_sync<NW>();
     for (int p = tid; p < G::P; p += NT) ptab[dqn_row_of(p, G::W)] = (uint16_t)dqn_bidx(p, G::W);
     conv_sync<NW>();
@@ -298,7 +304,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
         const int y = q / G::BW - 1, x = q % G::BW - 1;
         const bool in = c < G::NCELL0 && (unsigned)y < (unsigned)G::H && (unsigned)x < (unsigned)G::W && g * 8 < a.C;
         csrc[i] = in ? (y * G::W + x) * a.C + g * 8 : -1;
-        cdst[i] = c < G::NCELL0 ? G::OFF2 + g * G::CH + q * 16 : -1;
+        cdst[i] = c < G::NCELL0 ? G::OFF0 + g * G::CH + q * 16 : -1;
     }
     uint2 xin[NC];
     auto load_obs = [&](int64_t b) {
@@ -327,12 +333,12 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
         conv_sync<NW>();
         {   // conv1: CP -> 32
             f32x4 acc[MTW][NT1];
-            conv_mma<VR, CL, G::CP, G::K1S, NT1, 32>(lds, G::OFF2, gpos, toff1, a.w1, w * NT1, lane, acc);
+            conv_mma<VR, CL, G::CP, G::K1S, NT1, 32>(lds, G::OFF0, gpos, toff1, a.w1, w * NT1, lane, acc);
             conv_store_lds<VR, CL, NT1>(lds, G::OFF1, ptab + m0 * 16, w * NT1, lane, bias1, acc);
         }
         conv_sync<NW>();
-        // the input image is dead: restore a2's zero border
-        for (int i = tid; i < G::NBORDER * 8; i += NT) {
+        // the input image is dead: restore a2's zero border (overlaid case)
+        if constexpr (!G::SEP) for (int i = tid; i < G::NBORDER * 8; i += NT) {
             const int bi = i >> 3, chunk = i & 7;
             int q;
             if (bi < G::BW) q = bi;
@@ -366,7 +372,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
                 }
             }
         }
-        conv_sync<NW>();
+        if constexpr (!G::SEP) conv_sync<NW>();   // the next input image overwrites a2
     }
 }
 
@@ -631,7 +637,9 @@ extern "C" int snake_dqn_plan(const snake_dqn_cfg *cfg, snake_dqn_layout *out)
     out->fc1_w = 256ll * 64 * P16;
     out->fc2_w = 128ll * 256;
     out->act_per_obs = 64ll * P16;
-    out->lds_conv = (int32_t)(12 * ((NB + 15) / 16) * 256 + 2 * P16);
+    const int CH = ((NB + 15) / 16) * 256;                       // Geo<>::CH, Geo<>::SEP
+    const bool sep = 4 * ((12 + CP / 8) * CH + 2 * P16) <= 160 * 1024;
+    out->lds_conv = (int32_t)((sep ? 12 + CP / 8 : 12) * CH + 2 * P16);
     return SNAKE_OK;
 }
 
