@@ -399,6 +399,7 @@ struct FcArgs {
 // 16 lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, ...) then hit
 // distinct banks.
 constexpr int kFcRowsPerWave = 32;
+constexpr int kFcPlanes = 2;   // 32-wide k planes per stage (4: 128 KB of LDS, 89 VGPRs spilled)
 
 __device__ __forceinline__ int fc_tile_off(int plane, int n, int c)
 {
@@ -407,7 +408,8 @@ __device__ __forceinline__ int fc_tile_off(int plane, int n, int c)
 
 __global__ void __launch_bounds__(512) k_dqn_fc(const FcArgs a)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t bt[2][32768];
+    constexpr int KP = kFcPlanes;
+    __shared__ __attribute__((aligned(16))) uint8_t bt[2][KP * 16384];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int r16 = lane & 15, quad = lane >> 4, kq = 8 * quad;
     const int64_t row0 = (int64_t)blockIdx.x * kFcObs + wv * kFcRowsPerWave;
@@ -421,27 +423,30 @@ __global__ void __launch_bounds__(512) k_dqn_fc(const FcArgs a)
                                                        (int)(rows_here * a.K * 2), 0x00020000);
     const auto rs_w = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(a.w4), 0, 256 * a.K * 2, 0x00020000);
     const int va = ((wv * kFcRowsPerWave + r16) * a.K + kq) * 2;
-    // weight staging: slot = tid + 512 i -> row n = tid / 8 + 64 i, 16-byte chunk tid % 8 of the stage
-    const int vw = ((tid >> 3) * a.K + (tid & 7) * 8) * 2;
-    const int wdst = fc_tile_off((tid & 7) >> 2, tid >> 3, tid & 3);
-    const int nstage = a.K / 64;
-    u32x4 rb[4];
-    bf16x8 a0[2][2], a1[2][2];   // A of even / odd stages (no register copies between stages)
+    // weight staging: slot = tid + 512 i -> row n = tid / (4 KP) + (128 / KP) i, 16-byte
+    // chunk tid % (4 KP) of the stage
+    constexpr int CPR = 4 * KP, RSTEP = 512 / CPR, NLB = 2 * KP;
+    const int vw = ((tid / CPR) * a.K + (tid % CPR) * 8) * 2;
+    const int wdst = fc_tile_off((tid % CPR) >> 2, tid / CPR, tid & 3);
+    const int nstage = a.K / (32 * KP);
+    u32x4 rb[NLB];
+    bf16x8 a0[2][KP], a1[2][KP];   // A of even / odd stages (no register copies between stages)
     auto load_b = [&](int st) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) rb[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_w, vw, i * 64 * a.K * 2 + st * 128, 0);
+        for (int i = 0; i < NLB; i++)
+            rb[i] = __builtin_amdgcn_raw_buffer_load_b128(rs_w, vw, i * RSTEP * a.K * 2 + st * 64 * KP, 0);
     };
-    auto load_a = [&](int st, bf16x8 (&dst)[2][2]) {
+    auto load_a = [&](int st, bf16x8 (&dst)[2][KP]) {
 #pragma unroll
         for (int m = 0; m < 2; m++)
 #pragma unroll
-            for (int h = 0; h < 2; h++)
+            for (int h = 0; h < KP; h++)
                 dst[m][h] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                           rs_a, va, m * 16 * a.K * 2 + st * 128 + h * 64, 0));
+                                                           rs_a, va, m * 16 * a.K * 2 + st * 64 * KP + h * 64, 0));
     };
     auto store_b = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) *reinterpret_cast<u32x4 *>(&bt[buf][wdst + 4096 * i]) = rb[i];
+        for (int i = 0; i < NLB; i++) *reinterpret_cast<u32x4 *>(&bt[buf][wdst + RSTEP * 64 * i]) = rb[i];
     };
     f32x4 acc[2][16];
 #pragma unroll
@@ -450,10 +455,10 @@ __global__ void __launch_bounds__(512) k_dqn_fc(const FcArgs a)
         for (int n = 0; n < 16; n++) acc[m][n] = (f32x4)0.0f;
     // stage st: MFMAs on A(st) (in ra) and the LDS tile st & 1; then the tile
     // st + 1 (loaded a stage ago) goes to LDS and A / B of stage st + 2 are issued
-    auto stage = [&](int st, bf16x8 (&ra)[2][2]) {
+    auto stage = [&](int st, bf16x8 (&ra)[2][KP]) {
         const int buf = st & 1;
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < KP; h++) {
 #pragma unroll
             for (int n = 0; n < 16; n++) {
                 const bf16x8 bv = *reinterpret_cast<const bf16x8 *>(&bt[buf][fc_tile_off(h, n * 16 + r16, quad)]);
