@@ -1,15 +1,20 @@
 #!/usr/bin/env python3
 """Throughput of the batched multi-snake env step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Workload (BASELINE.json metric, config 3): 65 536 envs per GPU of 20x20 grids,
-4 snakes, vision_range=5, frame_stack=1, snake_length=3, default rewards,
-uniform random actions in {0,1,2} drawn up front on the device (seed 12345),
-all-done auto-reset inside the step. Env i is seeded with its GLOBAL index, so
-ranks hold disjoint shards of one big batch (weak scaling, no collective on the
-step path; the only collectives are the timing barrier and max-reduce).
+Workload (BASELINE.json metric, config 3 by default): 65 536 envs per GPU of
+20x20 grids, 4 snakes, vision_range=5, frame_stack=1, snake_length=3, default
+rewards, uniform random actions in {0,1,2} drawn up front on the device (seed
+12345), all-done auto-reset inside the step. Env i is seeded with its GLOBAL
+index, so ranks hold disjoint shards of one big batch (weak scaling, no
+collective on the step path; the only collectives are the timing barrier and
+max-reduce). --config picks BASELINE.json's other configs:
+  cfg2  4 096 envs/GPU, 20x20, 4 snakes, full-map observation
+  cfg3  65 536 envs/GPU, 20x20, 4 snakes, vision_range 5 (default)
+  cfg4  32 768 envs/GPU (262 144 over 8 GPUs), 20x20, 4 snakes, vision_range 5
+  cfg5  8 192 envs/GPU (65 536 over 8 GPUs), 40x40, 8 snakes, vision_range 5, frame_stack 4
 
 A step = one SnakeVecEnv.step() over the GPU's whole batch. The timed region is
 exactly K steps between barrier + synchronize on both sides; value = all envs of
@@ -26,16 +31,20 @@ The JSON line also carries:
                   frame reads) / its average duration, timed by the library's HIP
                   timing events on k_encode's own stream during the timed region
                   (snake_timing_enable; every --timing-stride-th step, default 8),
-                  against the 8 TB/s HBM peak; `traffic` =
-                  HBM bytes per k_encode launch from rocprofv3 PMC counters when
-                  profiles/pmc_traffic.json holds a measurement for this workload.
+                  against the 8 TB/s HBM peak; `traffic` is null (the HBM bytes of
+                  a launch come from rocprofv3 PMC passes, committed under
+                  profiles/, which a plain run cannot read).
   step_roofline -- the whole step against the same peak: B = S*h*w*8*fs +
                   (fs+1)*H*W + 10*S bytes per env-step x envs /
                   ms_per_step.
   kernels      -- average device ms per launch of each step kernel (same events).
   cpu_baseline -- rank 0 at N=1: the CPU restatement (oracle/, a C port of the
-                  reference SnakeEnv, 1 core) timed on a bounded sample of the same
-                  workload on this host.
+                  reference SnakeEnv) on every available host core (one process
+                  per core, at most 16: the box's CPU share), a bounded sample of
+                  the same workload, run BEFORE the GPU is touched; plus the
+                  reference-equivalent rate from profiles/cpu_ratio.json (the
+                  C-to-reference speed ratio measured where the reference runs,
+                  scripts/cpu_ratio.py).
 """
 import argparse
 import json
@@ -80,29 +89,49 @@ def encode_bytes(S, h, w, fs, H, W):
     return S * h * w * 8 * fs + fs * H * W
 
 
-def cpu_baseline(env_kw, num_snakes, seconds):
-    """CPU restatement of the reference step (oracle/, C, one core) on a bounded sample."""
-    import numpy as np
-    from oracle.snake_oracle import OracleEnv
-    n_env = 16
-    envs = [OracleEnv(seed=i, num_snakes=num_snakes, **env_kw) for i in range(n_env)]
-    for e in envs:
-        e.reset()
-    rs = np.random.RandomState(12345)
-    acts = rs.randint(0, 3, size=(4096, n_env, num_snakes))
-    steps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        a = acts[(steps // n_env) % 4096]
-        for i, e in enumerate(envs):
-            _, _, d, _ = e.step(a[i])
-            if d.all():
-                e.reset()
-        steps += n_env
-    el = time.perf_counter() - t0
-    return dict(value=round(steps / el, 1), unit='env-steps/s', cores=1, kind='port',
-                sample=f'{n_env} envs x {steps // n_env} steps incl. auto-resets, {el:.1f} s, '
-                       f'oracle/snake_oracle.c (serial C restatement of SnakeEnv.step/reset)')
+PRESETS = {   # BASELINE.json configs (per GPU)
+    'cfg2': dict(envs_per_gpu=4096, height=20, width=20, num_snakes=4, vision_range=0, frame_stack=1),
+    'cfg3': dict(envs_per_gpu=65536, height=20, width=20, num_snakes=4, vision_range=5, frame_stack=1),
+    'cfg4': dict(envs_per_gpu=32768, height=20, width=20, num_snakes=4, vision_range=5, frame_stack=1),
+    'cfg5': dict(envs_per_gpu=8192, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4),
+}
+
+
+def _cpu_worker(args):
+    env_kw, num_snakes, seconds, wid = args
+    import time as _t
+    from oracle.snake_oracle import rollout
+    n, steps, t0 = 0, 32, _t.perf_counter()
+    while _t.perf_counter() - t0 < seconds:
+        n += rollout(16, 1000 * wid, steps, act_seed=12345 + wid, num_snakes=num_snakes, **env_kw)
+        steps = min(2 * steps, 2048)
+    return n, _t.perf_counter() - t0
+
+
+def cpu_baseline(env_kw, num_snakes, seconds, ratio_key):
+    """The C restatement of the reference step (oracle/so_rollout: 16 envs per
+    process, random actions, all-done resets) on every available core, one
+    forked process per core. Runs before the GPU is initialised."""
+    import multiprocessing as mp
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    ctx = mp.get_context('fork')
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_worker, [(env_kw, num_snakes, seconds, w) for w in range(cores)])
+    n = sum(r[0] for r in res)
+    el = max(r[1] for r in res)
+    out = dict(value=round(n / el, 1), unit='env-steps/s', cores=cores, kind='port',
+               sample=f'{cores} processes x 16 envs, {n} env-steps incl. auto-resets in {el:.1f} s, '
+                      'oracle/snake_oracle.c so_rollout (serial C restatement of SnakeEnv.step/reset)')
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'cpu_ratio.json')) as fp:
+            r = json.load(fp)[ratio_key]
+        out['port_over_reference_1core'] = r['port_over_reference']
+        out['reference_equivalent'] = round(n / el / r['port_over_reference'], 1)
+        out['reference_1core_measured'] = r['reference_env_steps_per_s_1core']
+        out['ratio_source'] = 'profiles/cpu_ratio.json (scripts/cpu_ratio.py, measured in the build container)'
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def main():
@@ -110,24 +139,38 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=200)
-    ap.add_argument('--envs-per-gpu', type=int, default=65536)
-    ap.add_argument('--height', type=int, default=20)
-    ap.add_argument('--width', type=int, default=20)
-    ap.add_argument('--num-snakes', type=int, default=4)
-    ap.add_argument('--vision-range', type=int, default=5)
-    ap.add_argument('--frame-stack', type=int, default=1)
+    ap.add_argument('--config', choices=sorted(PRESETS), default='cfg3')
+    ap.add_argument('--envs-per-gpu', type=int, default=None)
+    ap.add_argument('--height', type=int, default=None)
+    ap.add_argument('--width', type=int, default=None)
+    ap.add_argument('--num-snakes', type=int, default=None)
+    ap.add_argument('--vision-range', type=int, default=None)
+    ap.add_argument('--frame-stack', type=int, default=None)
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--timing-stride', type=int, default=8,
                     help='bracket the kernels of every k-th timed step with timing events '
                          '(0: none; the events cost ~12 us per timed step)')
     args = ap.parse_args()
+    for k, v in PRESETS[args.config].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    env_kw = dict(height=args.height, width=args.width, snake_length=3,
+                  vision_range=args.vision_range or None, frame_stack=args.frame_stack)
+    S = args.num_snakes
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        key = None
+        if (args.height, args.width, S, args.frame_stack) == (20, 20, 4, 1) and args.vision_range in (0, 5):
+            key = 'cfg3_20x20_s4_vr5' if args.vision_range else 'cfg2_20x20_s4_full'
+        cpu = cpu_baseline(env_kw, S, args.cpu_seconds, key)
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
@@ -145,9 +188,6 @@ def main():
     per = args.envs_per_gpu
     n_total = per * world
     lo, hi = shard_range(n_total, world, rank)
-    env_kw = dict(height=args.height, width=args.width, snake_length=3,
-                  vision_range=args.vision_range or None, frame_stack=args.frame_stack)
-    S = args.num_snakes
     venv = SnakeVecEnv(hi - lo, num_snakes=S, device=device, seed=0, env_offset=lo, **env_kw)
     venv.reset()
     gen = torch.Generator(device=device)
@@ -200,21 +240,12 @@ def main():
     achieved = Be * encoded_per_launch / (enc_ms * 1e-3) / 1e9 if enc_ms > 0 else float('nan')
     value = n_total * args.steps / elapsed
     step_gbs = B * (hi - lo) / (elapsed / args.steps) / 1e9
-    workload = (f'cfg3: {per} envs/GPU x (20x20, 4 snakes, vision_range=5, frame_stack=1), '
-                'random actions, all-done auto-reset in the step'
-                if (args.height, args.width, S, args.vision_range, args.frame_stack) == (20, 20, 4, 5, 1)
-                else f'{per} envs/GPU x ({args.height}x{args.width}, {S} snakes, '
-                     f'vision_range={args.vision_range}, frame_stack={args.frame_stack})')
-    traffic = None
-    pmc_path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            key = f'k_encode_{args.height}x{args.width}_S{S}_vr{args.vision_range}_fs{args.frame_stack}_N{hi - lo}'
-            if key in pm:
-                traffic = pm[key]['hbm_bytes_per_launch']
-        except (OSError, ValueError, KeyError):
-            traffic = None
+    preset = PRESETS[args.config]
+    as_preset = all(getattr(args, k) == v for k, v in preset.items())
+    name = args.config if as_preset else 'custom'
+    workload = (f'{name}: {per} envs/GPU x ({args.height}x{args.width}, {S} snakes, '
+                f'vision_range={args.vision_range or None}, frame_stack={args.frame_stack}), '
+                'random actions, all-done auto-reset in the step')
     line = {
         'metric': METRIC,
         'value': round(value, 1),
@@ -234,7 +265,7 @@ def main():
                    'snake_length': 3, 'parallelism': f'env-shard x{world}'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                     'traffic': traffic, 'kernel': 'k_encode', 'kernel_ms': round(enc_ms, 4),
+                     'traffic': None, 'kernel': 'k_encode', 'kernel_ms': round(enc_ms, 4),
                      'algorithmic_bytes_per_launch': round(Be * encoded_per_launch),
                      'bytes_per_encoded_env': Be},
         'step_roofline': {'achieved': round(step_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -247,8 +278,7 @@ def main():
                         if n_timed else None),
         'cpu_baseline': None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(env_kw, S, args.cpu_seconds)
+    line['cpu_baseline'] = cpu
     if rank == 0:
         print(json.dumps(line), flush=True)
     if distributed:

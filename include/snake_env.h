@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 7
+#define SNAKE_ABI_VERSION 8
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -62,7 +62,8 @@ typedef struct {
     int64_t snake;      /* int32  [N][S][4]              packed snake records */
     int64_t body;       /* uint8  [N][S][ring_cap]       direction deques (rings) */
     int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos,
-                                                         spawn-ahead status (0 none, 1 partial, 2 ready) */
+                                                         spawn-ahead status (0 none, 1 partial, 2 ready),
+                                                         spawn failure (1: the last reset gave up, below) */
     int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */
     int64_t stats;      /* double [N][4][S]              episode scores/steps/fruits/kills */
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
@@ -71,15 +72,17 @@ typedef struct {
                                                          u16 draw record fits LDS (2*n_cand <= 36 KB) */
     int64_t spawn;      /* uint32 [N][656]               spawn-ahead record: MT key, MT pos and the
                                                          S spawn-pose indices of the env's next reset */
-    int64_t resetq;     /* int32  [2][64][cap] + [2][160] sharded auto-reset and spawn-ahead queues
-                                                         + per-step counters */
+    int64_t resetq;     /* int32  [2][64][cap] + [160]   sharded auto-reset and spawn-ahead queues
+                                                         + the step's counters (zero between steps) */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */
     int64_t rew;        /* double [N][S] */
     int64_t done;       /* uint8  [N][S] */
     int64_t ep_done;    /* uint8  [N]                    1 when the step ended the episode */
-    int64_t rank;       /* int32  [N][S]                 info['rank'] (valid where ep_done) */
-    int64_t ep_stats;   /* double [N][4][S]              info episode_* (valid where ep_done) */
-    int64_t err;        /* int32  [N]                    1 = invalid action (reference KeyError) */
+    int64_t rank;       /* int32  [N][S]                 info['rank'] where ep_done, else 0 */
+    int64_t ep_stats;   /* double [N][4][S]              info episode_* where ep_done, else 0 */
+    int64_t err;        /* int32  [N]                    1 = invalid action (reference KeyError: the
+                                                         env is left unchanged, its rew/done are 0);
+                                                         2 = its auto-reset gave up (below) */
     int64_t n_cand;     /* rows of the spawn-pose table */
     int32_t obs_h, obs_w, obs_c;
     int32_t grid_stride, ring_cap;
@@ -110,7 +113,11 @@ typedef struct {        /* device output buffers of one step/reset */
 } snake_out;
 
 /* Validate cfg and compute buffer sizes. Replaces SnakeEnv.__init__'s checks and
- * observation_space shape (snake_env.py:58-129). */
+ * observation_space shape (snake_env.py:58-129). Also rejects boards on which S
+ * random spawn poses are disjoint in fewer than 2e-4 of the draws (estimated by
+ * sampling): the reference's _generate_snakes retries forever (:576-589), a reset
+ * here gives up after 2^16 permutations -- sets env word 5 (and err = 2 for an
+ * auto-reset) -- which the bound keeps below ~2e-6 per reset. */
 int snake_plan(const snake_cfg *cfg, int64_t num_envs, snake_layout *out);
 
 /* Host-side spawn-pose table = dfs_sweep_empty(make_grid(H, W), L) in reference

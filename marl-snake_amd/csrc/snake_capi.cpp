@@ -160,19 +160,83 @@ static int64_t build_table(int H, int W, int L, std::vector<int16_t> *out)
     return d.count;
 }
 
-// n_cand per (H, W, L), memoised: snake_step/snake_reset re-plan on every call.
-static int64_t cached_count(int H, int W, int L)
+// Spawn-pose table per (H, W, L), memoised (snake_step/snake_reset re-plan on
+// every call), and per S the probability that S poses drawn as
+// permutation(n_cand)[:S] are pairwise disjoint (_generate_snakes' retry test,
+// snake_env.py:576-589), estimated once by sampling.
+struct PoseTable {
+    int64_t n = 0;
+    std::vector<int16_t> cells;
+    std::map<int, double> p_disjoint;
+};
+
+static std::mutex g_table_mu;
+
+static PoseTable &pose_table(int H, int W, int L)   // g_table_mu held
 {
-    static std::mutex mu;
-    static std::map<std::tuple<int, int, int>, int64_t> memo;
-    std::lock_guard<std::mutex> lock(mu);
+    static std::map<std::tuple<int, int, int>, PoseTable> memo;
     auto key = std::make_tuple(H, W, L);
     auto it = memo.find(key);
     if (it != memo.end()) return it->second;
-    int64_t n = build_table(H, W, L, nullptr);
-    memo[key] = n;
-    return n;
+    PoseTable t;
+    t.n = build_table(H, W, L, &t.cells);
+    return memo.emplace(key, std::move(t)).first->second;
 }
+
+static int64_t cached_count(int H, int W, int L)
+{
+    std::lock_guard<std::mutex> lock(g_table_mu);
+    return pose_table(H, W, L).n;
+}
+
+// Monte-Carlo estimate (fixed seed, so deterministic) of P(S uniformly drawn
+// distinct poses share no cell): up to 2e5 samples, stopping once 400 disjoint
+// draws have been seen.
+static double disjoint_prob(int H, int W, int L, int S)
+{
+    std::lock_guard<std::mutex> lock(g_table_mu);
+    PoseTable &t = pose_table(H, W, L);
+    auto it = t.p_disjoint.find(S);
+    if (it != t.p_disjoint.end()) return it->second;
+    double p = 1.0;
+    if (S > 1 && t.n >= S) {
+        std::vector<uint32_t> stamp((size_t)H * W, 0u);
+        uint64_t x = 0x9e3779b97f4a7c15ull;
+        auto next = [&x]() {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            return x;
+        };
+        int64_t hits = 0, m = 0;
+        int64_t pick[kMaxSnakes];
+        for (m = 1; m <= 200000 && hits < 400; m++) {
+            bool ok = true;
+            for (int k = 0; k < S; k++) {
+                int64_t v;
+                bool dup;
+                do {
+                    v = (int64_t)(next() % (uint64_t)t.n);
+                    dup = false;
+                    for (int j = 0; j < k; j++) dup |= pick[j] == v;
+                } while (dup);
+                pick[k] = v;
+                for (int i = 0; i < L && ok; i++) {
+                    uint32_t &c = stamp[t.cells[(size_t)v * L + i]];
+                    ok = c != (uint32_t)m;
+                    c = (uint32_t)m;
+                }
+            }
+            hits += ok;
+        }
+        p = (double)hits / (double)(m - 1);
+    }
+    t.p_disjoint[S] = p;
+    return p;
+}
+
+// Boards on which S disjoint spawn poses are this rare are rejected: a reset
+// gives up after 2^16 permutations (snake_kernels.hip do_reset), which at this
+// probability happens for fewer than ~2e-6 of the resets.
+constexpr double kMinDisjoint = 2e-4;
 
 int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
 {
@@ -209,7 +273,7 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
         const int64_t E = kWave / (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
         const int64_t blocks = (N + E - 1) / E;
         const int64_t cap = (blocks + kQShards - 1) / kQShards * E;
-        o->resetq = (2 * kQShards * cap + 2 * kQCounters) * 4;
+        o->resetq = (2 * kQShards * cap + kQCounters) * 4;
     }
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
@@ -225,6 +289,13 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     }
     if (o->n_cand < S) {
         set_error("only %lld spawn poses for %lld snakes", (long long)o->n_cand, (long long)S);
+        return SNAKE_E_CONFIG;
+    }
+    const double pd = disjoint_prob(c->height, c->width, c->snake_length, (int)S);
+    if (pd < kMinDisjoint) {
+        set_error("%dx%d board too crowded: %lld snakes of length %d are disjoint in only "
+                  "%.2g of the spawn draws (the reference would retry ~%.0f permutations per reset)",
+                  c->height, c->width, (long long)S, c->snake_length, pd, pd > 0 ? 1.0 / pd : 1e30);
         return SNAKE_E_CONFIG;
     }
     return SNAKE_OK;
@@ -420,16 +491,7 @@ int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, co
     if ((rc = check_state(k, st, true))) return rc;
     if ((rc = check_out(out, true))) return rc;
     if (!actions) { set_error("actions is NULL"); return SNAKE_E_ARG; }
-    // The auto-reset queue has two counters used on alternate steps (each step's
-    // logic kernel zeroes the other one); the parity is per state, kept here.
-    static std::mutex mu;
-    static std::map<const void *, unsigned> ticks;
-    unsigned parity;
-    {
-        std::lock_guard<std::mutex> lock(mu);
-        parity = ticks[st->resetq]++ & 1u;
-    }
-    return launch_step(k, *st, actions, *out, (int)parity, stream);
+    return launch_step(k, *st, actions, *out, stream);
 }
 
 int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,

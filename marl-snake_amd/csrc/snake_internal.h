@@ -19,10 +19,12 @@ constexpr int kStageMax = 8192;     // bytes of staged observation per encode gr
 constexpr int kSpawnStride = 656;   // u32 words per spawn-ahead record: key, pos, poses
 constexpr int kSpawnPos = 624;      // record word: MT position after the recorded attempts
 constexpr int kSpawnSel = 625;      // record words [625, 625 + S): spawn-pose indices
-constexpr int kQCounters = 160;     // per-parity queue counters: 64 reset, 64 spawn, claim
+constexpr int kQCounters = 160;     // queue counters: 64 reset, 64 spawn, claim, worker exits
+constexpr int kQClaim = 128;        // counter word: next job index claimed by a free worker
+constexpr int kQExit = 129;         // counter word: k_autoreset workers finished
 
 // env record words
-enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4 };
+enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, ENV_FAIL = 5 };
 // spawn-ahead status (env word ENV_SPAWN)
 enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2 };
 
@@ -70,7 +72,7 @@ int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_
 int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, const snake_out &o,
                  void *stream);
 int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, const snake_out &o,
-                int parity, void *stream);
+                void *stream);
 int launch_render(const KCfg &k, const snake_state &st, const uint8_t *palette, uint8_t *rgb,
                   void *stream);
 

@@ -737,15 +737,20 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     const int S = c.S, L = c.L, W = c.W, SL = S * L;
     const int sk = lane / L, si = lane - sk * L;
     int cell = -1;
+    bool failed = false;
     if (spst == SPAWN_READY) {
         const uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
         if (lane < SL) cell = (int)st.cand[(int64_t)rec[kSpawnSel + sk] * L + si];
     } else {
         // The reference retries forever; a board too crowded for S disjoint spawn
-        // poses would hang the wave, so give up after 2^16 permutations.
+        // poses would hang the wave, so give up after 2^16 permutations and flag
+        // the env (env word ENV_FAIL; snake_plan rejects boards where that is
+        // likelier than ~1e-6 per reset)
         int q[MS];
-        for (int attempt = 0; attempt < (1 << 16); attempt++)
-            if (spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, attempt, q, cell, lane)) break;
+        bool ok = false;
+        for (int attempt = 0; attempt < (1 << 16) && !ok; attempt++)
+            ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, attempt, q, cell, lane);
+        failed = !ok;
     }
     // make_grid (grid_util.py:14-20), then paint (:138-144)
     for (int x = lane; x < c.HW; x += kWave) {
@@ -794,6 +799,8 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         er.x = S; er.y = 0; er.z = c.fs - 1; er.w = mt.pos;
         *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = er;
         if (spst != SPAWN_NONE) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = SPAWN_NONE;   // record used up
+        st.env[(int64_t)e * kEnvRec + ENV_FAIL] = failed ? 1 : 0;
+        if (failed && o.err) o.err[e] = 2;
     }
     if (lane < 4 * S) st.stats[(int64_t)e * 4 * S + lane] = 0.0;   // _reset_epi_stats
     mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
@@ -837,7 +844,7 @@ __device__ __forceinline__ void stage_to_lds(uint8_t *dst, const uint8_t *src, i
 template <int MS>
 __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c, const snake_state st,
                                                               const int8_t *__restrict__ actions,
-                                                              const snake_out o, int parity)
+                                                              const snake_out o)
 {
     constexpr int G = MS, E = kWave / MS;
     constexpr uint32_t gmask = (1u << G) - 1u;
@@ -853,9 +860,8 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // per-env respawn scratch: G * kRespawnT tempered raws, G chosen cells
     uint32_t *rawbuf = reinterpret_cast<uint32_t *>(lds + E * stride + 2 * kMaxFruits) + g * (G * kRespawnT);
     uint16_t *cellbuf = reinterpret_cast<uint16_t *>(lds + E * stride + 2 * kMaxFruits + E * G * kRespawnT * 4) + g * G;
-    int *qcnt = st.resetq + 2 * kQShards * c.q_cap;                   // [2][kQCounters]
-    if (blockIdx.x == 0)                                              // next step's counters
-        for (int q = lane; q < kQCounters; q += kWave) qcnt[(parity ^ 1) * kQCounters + q] = 0;
+    // queue counters (zero between steps: the last k_autoreset worker re-zeroes them)
+    int *qcnt = st.resetq + 2 * kQShards * c.q_cap;
     LSTAMP(40);
     auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
@@ -984,7 +990,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && ep_end) : 0ull;
     const int shard = blockIdx.x % kQShards;
     int qbase = 0;
-    if (qm && lane == 0) qbase = atomicAdd(&qcnt[parity * kQCounters + shard], __popcll(qm));
+    if (qm && lane == 0) qbase = atomicAdd(&qcnt[shard], __popcll(qm));
 
     // rewards, fp64 in the reference order (:354-370)
     const bool counted = death || alive;   // not previously dead
@@ -1159,7 +1165,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
                          __popc(am) <= c.spawn_thr;
     const unsigned long long pm = __ballot(spawn_q && k == 0);
     int pbase = 0;
-    if (pm && lane == 0) pbase = atomicAdd(&qcnt[parity * kQCounters + kQShards + shard], __popcll(pm));
+    if (pm && lane == 0) pbase = atomicAdd(&qcnt[kQShards + shard], __popcll(pm));
 
     LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
@@ -1170,9 +1176,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         s2 = s2 + msk * (counted ? (double)eat : 0.0);
         s3 = s3 + msk * (counted ? (double)kills : 0.0);
     }
-    if (live) {
-        o.rew[(int64_t)e * S + k] = rew;
-        o.done[(int64_t)e * S + k] = (uint8_t)fd;
+    if (isn) {   // an env rejected for an invalid action reports reward 0, not done
+        o.rew[(int64_t)e * S + k] = live ? rew : 0.0;
+        o.done[(int64_t)e * S + k] = (uint8_t)(live ? fd : 0);
     }
     if (env_ok && k == 0) {
         o.ep_done[e] = ep_end ? 1 : 0;
@@ -1191,14 +1197,13 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     LSTAMP(49);
     int rank = 1;
     for (int j = 0; j < S; j++) rank += (__shfl(s0, gb + j) > s0);
-    if (ep_end) {
-        if (isn) {
-            o.rank[(int64_t)e * S + k] = rank;
-            double *es = o.ep_stats + (int64_t)e * 4 * S;
-            es[k] = s0; es[S + k] = s1; es[2 * S + k] = s2; es[3 * S + k] = s3;
-        }
-        s0 = s1 = s2 = s3 = 0.0;                                   // _reset_epi_stats
+    if (isn) {           // the episode summary where it ended, zeros elsewhere
+        o.rank[(int64_t)e * S + k] = ep_end ? rank : 0;
+        double *es = o.ep_stats + (int64_t)e * 4 * S;
+        es[k] = ep_end ? s0 : 0.0; es[S + k] = ep_end ? s1 : 0.0;
+        es[2 * S + k] = ep_end ? s2 : 0.0; es[3 * S + k] = ep_end ? s3 : 0.0;
     }
+    if (ep_end) s0 = s1 = s2 = s3 = 0.0;                           // _reset_epi_stats
     if (live) { sp[k] = s0; sp[S + k] = s1; sp[2 * S + k] = s2; sp[3 * S + k] = s3; }
 
     LSTAMP(46);
@@ -1270,14 +1275,13 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
 // k_encode encodes every other env's stacked frames (bandwidth-bound, few
 // registers: full occupancy).
 template <int MS>
-__global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_state st, const snake_out o,
-                                                  int parity)
+__global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_state st, const snake_out o)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
     // the shard counts of both queues, prefix-summed: queue index idx lives in
     // the shard whose [excl, incl) holds it
-    int *qc = st.resetq + 2 * kQShards * c.q_cap + parity * kQCounters;
+    int *qc = st.resetq + 2 * kQShards * c.q_cap;
     const int cnt = qc[lane], pcnt = qc[kQShards + lane];
     const int incl = wave_scan(cnt, lane), excl = incl - cnt;
     const int pincl = wave_scan(pcnt, lane), pexcl = pincl - pcnt;
@@ -1313,9 +1317,16 @@ __global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_stat
             if (j < 128) OBSPROF(640 + j, lane);
         }
         int nx = 0;
-        if (lane == 0) nx = atomicAdd(&qc[2 * kQShards], 1);
+        if (lane == 0) nx = atomicAdd(&qc[kQClaim], 1);
         idx = (int)gridDim.x + bcast(nx, 0);
     }
+    // the last worker to finish re-zeroes the step's counters for the next step
+    // (every worker has read its counts and made its last claim before its exit
+    // count: the device state needs no host-side step parity)
+    int last = 0;
+    if (lane == 0) last = atomicAdd(&qc[kQExit], 1) == (int)gridDim.x - 1;
+    if (bcast(last, 0))
+        for (int q = lane; q < kQCounters; q += kWave) qc[q] = 0;
 }
 
 __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state st, const snake_out o)
@@ -1479,6 +1490,31 @@ struct TimedLaunch {
     }
 };
 
+// Every launch runs with the caller stream's device current: the side stream and
+// events are created on it, and a SnakeVecEnv on cuda:1 works whatever device the
+// calling thread has current (restored on return).
+struct DeviceGuard {
+    int dev = -1, prev = -1;
+    explicit DeviceGuard(hipStream_t s)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) { set_error("hipGetDevice failed"); return; }
+        if (s == nullptr) { dev = prev; return; }
+        if (hipStreamGetDevice(s, &dev) != hipSuccess) {
+            set_error("hipStreamGetDevice failed");
+            dev = -1;
+            return;
+        }
+        if (dev != prev && hipSetDevice(dev) != hipSuccess) {
+            set_error("hipSetDevice(%d) failed", dev);
+            dev = -1;
+        }
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0 && dev >= 0 && dev != prev) (void)hipSetDevice(prev);
+    }
+};
+
 // ---------------------------------------------------------------- launchers
 static int check_launch(const char *what)
 {
@@ -1494,6 +1530,8 @@ int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_
                 void *stream)
 {
     const int threads = 256, blocks = (k.N + threads - 1) / threads;
+    DeviceGuard dg((hipStream_t)stream);
+    if (dg.dev < 0) return SNAKE_E_LAUNCH;
     hipLaunchKernelGGL(k_seed, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, k, st,
                        base_seed, (long long)env_offset);
     return check_launch("k_seed");
@@ -1504,6 +1542,8 @@ int launch_render(const KCfg &k, const snake_state &st, const uint8_t *palette, 
 {
     RenderPal pal;
     memcpy(pal.rgb, palette, sizeof(pal.rgb));
+    DeviceGuard dg((hipStream_t)stream);
+    if (dg.dev < 0) return SNAKE_E_LAUNCH;
     const long long quads = ((long long)k.N * k.HW + 3) / 4;
     const int threads = 256;
     const long long blocks = (quads + threads - 1) / threads;
@@ -1516,6 +1556,8 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
                  void *stream)
 {
     const dim3 grid(k.link_in_lds ? k.N : k.reset_slots), block(kWave);
+    DeviceGuard dg((hipStream_t)stream);
+    if (dg.dev < 0) return SNAKE_E_LAUNCH;
     TimedLaunch tl("k_reset", (hipStream_t)stream);
     if (k.S <= 4) hipLaunchKernelGGL(k_reset<4>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
     else if (k.S <= 8) hipLaunchKernelGGL(k_reset<8>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
@@ -1538,15 +1580,10 @@ struct SideCtx {
 // cheaper in isolation).
 constexpr unsigned kJoinFlags = hipEventDisableTiming | hipEventDisableSystemFence;
 
-static int side_ctx(hipStream_t main, SideCtx *out)
+static int side_ctx(hipStream_t main, int dev, SideCtx *out)
 {
     static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, SideCtx> ctx;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) {
-        set_error("hipGetDevice failed");
-        return SNAKE_E_LAUNCH;
-    }
     std::lock_guard<std::mutex> g(mu);
     auto it = ctx.find({dev, main});
     if (it == ctx.end()) {
@@ -1564,18 +1601,20 @@ static int side_ctx(hipStream_t main, SideCtx *out)
 }
 
 int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, const snake_out &o,
-                int parity, void *stream)
+                void *stream)
 {
     KCfg k = k0;
     k.diag = g_timing ? 1 : 0;
     const hipStream_t sm = (hipStream_t)stream;
+    DeviceGuard dg(sm);
+    if (dg.dev < 0) return SNAKE_E_LAUNCH;
     const int ms = k.S <= 4 ? 4 : (k.S <= 8 ? 8 : 16), epw = kWave / ms;   // envs per k_logic wave
     const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits + epw * ms * kRespawnT * 4 + epw * ms * 2;
     const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
     TimedLaunch t1("k_logic", sm);
-    if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, k, st, actions, o, parity);
-    else if (ms == 8) hipLaunchKernelGGL(k_logic<8>, gl, block, lds_logic, sm, k, st, actions, o, parity);
-    else hipLaunchKernelGGL(k_logic<16>, gl, block, lds_logic, sm, k, st, actions, o, parity);
+    if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, k, st, actions, o);
+    else if (ms == 8) hipLaunchKernelGGL(k_logic<8>, gl, block, lds_logic, sm, k, st, actions, o);
+    else hipLaunchKernelGGL(k_logic<16>, gl, block, lds_logic, sm, k, st, actions, o);
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;
@@ -1591,7 +1630,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     // side stream; join before return. SNAKE_ENCODE_ON_MAIN=1 swaps the two
     // (A/B probe: 0.155 vs 0.135 ms per step for cfg3).
     SideCtx sc;
-    if ((rc = side_ctx(sm, &sc))) return rc;
+    if ((rc = side_ctx(sm, dg.dev, &sc))) return rc;
     if (hipEventRecord(sc.fork, sm) != hipSuccess || hipStreamWaitEvent(sc.side, sc.fork, 0) != hipSuccess) {
         set_error("fork to the side stream failed");
         return SNAKE_E_LAUNCH;
@@ -1600,9 +1639,9 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     const hipStream_t s_res = resets_main ? sm : sc.side, s_enc = resets_main ? sc.side : sm;
     auto launch_resets = [&]() {
         TimedLaunch t2("k_autoreset", s_res);
-        if (k.S <= 4) hipLaunchKernelGGL(k_autoreset<4>, gr, block, k.lds_bytes, s_res, k, st, o, parity);
-        else if (k.S <= 8) hipLaunchKernelGGL(k_autoreset<8>, gr, block, k.lds_bytes, s_res, k, st, o, parity);
-        else hipLaunchKernelGGL(k_autoreset<16>, gr, block, k.lds_bytes, s_res, k, st, o, parity);
+        if (k.S <= 4) hipLaunchKernelGGL(k_autoreset<4>, gr, block, k.lds_bytes, s_res, k, st, o);
+        else if (k.S <= 8) hipLaunchKernelGGL(k_autoreset<8>, gr, block, k.lds_bytes, s_res, k, st, o);
+        else hipLaunchKernelGGL(k_autoreset<16>, gr, block, k.lds_bytes, s_res, k, st, o);
         t2.close();
         return check_launch("k_autoreset");
     };

@@ -100,6 +100,8 @@ class SnakeEnv:
         obs = self._vec.reset()
         out = obs[0].cpu().numpy()
         self._pull_rng()
+        if int(self._vec.spawn_failures()[0]):
+            raise RuntimeError('reset gave up after 2^16 spawn permutations without disjoint snakes')
         self.frame_buffer = []
         return np.array(out, dtype=np.uint8)
 

@@ -78,8 +78,9 @@ class SnakeVecEnv:
             self.ctr.data_ptr(), self.stats.data_ptr(), self.mt.data_ptr(), self.cand.data_ptr(),
             self.jscratch.data_ptr() if self.jscratch is not None else None,
             self.spawn.data_ptr(), self.resetq.data_ptr())
-        check(L.snake_seed(ctypes.byref(self.cfg), ctypes.byref(self._state), N, self.seed_base,
-                           self.env_offset, self._stream()))
+        with torch.cuda.device(dev):
+            check(L.snake_seed(ctypes.byref(self.cfg), ctypes.byref(self._state), N, self.seed_base,
+                               self.env_offset, self._stream()))
 
         self.single_action_space = spaces.Discrete(self.action_n)
         self.single_observation_space = spaces.Box(0, 255, self.obs_shape, np.uint8)
@@ -130,9 +131,10 @@ class SnakeVecEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.uint8).reshape(self.num_envs).contiguous()
-        check(self._L.snake_reset(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
-                                ctypes.c_void_p(m.data_ptr()) if m is not None else None,
-                                ctypes.byref(so), self._stream()))
+        with torch.cuda.device(self.device):
+            check(self._L.snake_reset(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+                                      ctypes.c_void_p(m.data_ptr()) if m is not None else None,
+                                      ctypes.byref(so), self._stream()))
         self._keep = m
         self._reset_done = True
         return out['obs']
@@ -144,23 +146,31 @@ class SnakeVecEnv:
         Returns (obs uint8 (N,S,h,w,C), rewards float64 (N,S), dones bool (N,S), info)
         with info tensors 'episode_done' (N,), 'rank' (N,S) and 'episode_scores',
         'episode_steps', 'episode_fruits', 'episode_kills' (N,S), meaningful where
-        episode_done; 'error' (N,) flags envs whose step was rejected for an invalid
-        action (the reference's KeyError; such an env is left unchanged).
+        episode_done (zeros elsewhere); 'error' (N,) flags envs whose step was rejected
+        for an invalid action (1: the reference's KeyError; such an env is left
+        unchanged and reports reward 0 and done False) or whose auto-reset gave up
+        finding disjoint spawn poses (2, see spawn_failures()).
         All outputs are freshly allocated every call."""
         if not self._reset_done:
             raise RuntimeError('call reset() before step()')
+        torch = _torch()
         a = self._actions(actions)
         out, so = self._new_out()
-        check(self._L.snake_step(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
-                               ctypes.c_void_p(a.data_ptr()), ctypes.byref(so), self._stream()))
+        with torch.cuda.device(self.device):
+            check(self._L.snake_step(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+                                     ctypes.c_void_p(a.data_ptr()), ctypes.byref(so), self._stream()))
         self._keep = a
         info = {'episode_done': out['ep_done'], 'rank': out['rank'],
                 'episode_scores': out['ep_stats'][:, 0], 'episode_steps': out['ep_stats'][:, 1],
                 'episode_fruits': out['ep_stats'][:, 2], 'episode_kills': out['ep_stats'][:, 3],
                 'error': out['err']}
         if self.strict and bool(out['err'].any()):
-            bad = out['err'].nonzero().flatten().tolist()
-            raise KeyError(f'invalid action for an alive snake in envs {bad[:8]}')
+            err = out['err']
+            bad = (err == 1).nonzero().flatten().tolist()
+            if bad:
+                raise KeyError(f'invalid action for an alive snake in envs {bad[:8]}')
+            raise RuntimeError(f'auto-reset gave up placing disjoint snakes in envs '
+                               f'{(err == 2).nonzero().flatten().tolist()[:8]}')
         return out['obs'], out['rew'], out['done'], info
 
     def render_rgb(self):
@@ -172,9 +182,10 @@ class SnakeVecEnv:
         if self._palette is None:
             from .core.render import palette
             self._palette = np.ascontiguousarray(palette())
-        check(self._L.snake_render_rgb(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
-                                       self._palette.ctypes.data_as(ctypes.c_void_p),
-                                       ctypes.c_void_p(rgb.data_ptr()), self._stream()))
+        with torch.cuda.device(self.device):
+            check(self._L.snake_render_rgb(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+                                           self._palette.ctypes.data_as(ctypes.c_void_p),
+                                           ctypes.c_void_p(rgb.data_ptr()), self._stream()))
         return rgb
 
     # --------------------------------------------------------- introspection
@@ -188,6 +199,54 @@ class SnakeVecEnv:
         cur = self.env_rec.view(self.num_envs, 8)[:, 2].long()
         g = ring[torch.arange(self.num_envs, device=self.device), cur][:, :H * W]
         return g.reshape(self.num_envs, H, W)
+
+    def spawn_failures(self):
+        """(N,) int32: 1 where the env's last reset gave up after 2^16 spawn
+        permutations without S disjoint poses (its snakes may overlap). snake_plan
+        rejects boards where that is likelier than ~2e-6 per reset."""
+        return self.env_rec.view(self.num_envs, 8)[:, 5]
+
+    # ------------------------------------------------------- snapshot/restore
+    _STATE_BUFFERS = ('grid', 'snake', 'body', 'env_rec', 'ctr', 'stats', 'mt', 'spawn')
+
+    def state_dict(self, device=None):
+        """Snapshot of the whole batch: every persistent state buffer of
+        snake_layout (grid ring, snake records, body rings, env records, crop
+        centres, episode statistics, MT19937 keys, spawn-ahead records) copied
+        (to `device`, default: this env's device) plus the configuration it
+        belongs to. The step's queues and link tables are transient (empty
+        between steps) and not saved. load_state_dict() on this or a fresh
+        SnakeVecEnv of the same configuration continues bit-identically; the
+        tensors can be torch.save()d beside a learner checkpoint
+        (train_dqn.py:356-383)."""
+        torch = _torch()
+        dev = torch.device(device) if device is not None else self.device
+        torch.cuda.current_stream(self.device).synchronize()
+        sd = {k: getattr(self, k).detach().to(dev, copy=True) for k in self._STATE_BUFFERS}
+        sd['meta'] = self._snapshot_meta()
+        return sd
+
+    def _snapshot_meta(self):
+        lay = self.layout
+        return dict(abi=int(self._L.snake_abi_version()), num_envs=self.num_envs,
+                    cfg=[getattr(self.cfg, f) for f, _ in self.cfg._fields_ if f != 'spawn_ahead'],
+                    sizes=[int(getattr(lay, k)) for k in ('grid', 'snake', 'body', 'env', 'ctr', 'stats',
+                                                          'mt', 'spawn')],
+                    seed=self.seed_base, env_offset=self.env_offset, reset_done=self._reset_done)
+
+    def load_state_dict(self, sd):
+        """Restore a state_dict() snapshot (same configuration and num_envs,
+        checked); the next step continues exactly where the snapshot was taken."""
+        torch = _torch()
+        mine, theirs = self._snapshot_meta(), sd['meta']
+        for key in ('abi', 'num_envs', 'cfg', 'sizes'):
+            if mine[key] != theirs[key]:
+                raise ValueError(f'snapshot does not match this env: {key} {theirs[key]} != {mine[key]}')
+        with torch.cuda.device(self.device):
+            for k in self._STATE_BUFFERS:
+                getattr(self, k).copy_(sd[k].to(self.device))
+        self.seed_base, self.env_offset = theirs['seed'], theirs['env_offset']
+        self._reset_done = bool(theirs['reset_done'])
 
     def alive_counters(self):
         return self.env_rec.view(self.num_envs, 8)[:, 0]

@@ -622,9 +622,14 @@ int so_step(so_env *e, const int32_t *actions, uint8_t *obs, double *rews, uint8
     e->episode_length += 1;                             /* :392-394 */
     if ((double)e->episode_length >= c->max_episode_steps)
         for (int k = 0; k < S; k++) dn[k] = 1;
-    int all = 1;
-    for (int k = 0; k < S; k++) { dones[k] = dn[k]; all &= dn[k]; }
-    if (!all) return 0;
+    /* _done_fn (:416-417): all(dones); CoopSnakeEnv._done_fn any(dones), and its
+     * step() then reports every done True (coop_snake_env.py:14-22) -- after the
+     * statistics above were masked with the per-snake dones */
+    int all = 1, any = 0;
+    for (int k = 0; k < S; k++) { all &= dn[k]; any |= dn[k]; }
+    const int ended = c->coop ? any : all;
+    for (int k = 0; k < S; k++) dones[k] = (c->coop && ended) ? 1 : dn[k];
+    if (!ended) return 0;
     /* :396-412 competition rank on descending unique scores */
     if (info) {
         int assigned[16] = {0};
@@ -702,4 +707,46 @@ void so_rng_permutation(uint32_t seed, int64_t n, int64_t *out, uint32_t *next)
     so_mt st; mt_seed(&st, seed);
     mt_permutation(&st, n, out);
     *next = mt_next(&st);
+}
+
+/* CPU baseline driver (bench.py cpu_baseline, scripts/cpu_ratio.py): n_env envs
+ * seeded seed..seed+n_env-1, stepped round-robin for `steps` steps each with
+ * uniform random actions in {0,1,2} (xorshift32, act_seed), reset whenever all
+ * dones are True (the vector-env auto-reset, wrappers.py:141-143). Returns the
+ * env-steps run, or -1. */
+int64_t so_rollout(const so_cfg *cfg, int32_t n_env, uint32_t seed, int64_t steps, uint32_t act_seed)
+{
+    if (n_env < 1 || n_env > 4096) return -1;
+    so_env **envs = (so_env **)calloc((size_t)n_env, sizeof *envs);
+    if (!envs) return -1;
+    int64_t n = -1;
+    uint8_t *obs = NULL;
+    for (int i = 0; i < n_env; i++)
+        if (!(envs[i] = so_create(cfg, seed + (uint32_t)i))) goto done;
+    obs = (uint8_t *)malloc((size_t)so_obs_size(envs[0]));
+    if (!obs) goto done;
+    for (int i = 0; i < n_env; i++) so_reset(envs[i], obs);
+    uint32_t x = act_seed ? act_seed : 12345u;
+    int32_t act[16];
+    double rews[16];
+    uint8_t dones[16];
+    n = 0;
+    for (int64_t t = 0; t < steps; t++) {
+        for (int i = 0; i < n_env; i++) {
+            for (int k = 0; k < cfg->num_snakes; k++) {
+                x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+                act[k] = (int32_t)(x % 3u);
+            }
+            int rc = so_step(envs[i], act, obs, rews, dones, NULL);
+            int all = 1;
+            for (int k = 0; k < cfg->num_snakes; k++) all &= dones[k];
+            if (rc >= 0 && all) so_reset(envs[i], obs);
+            n++;
+        }
+    }
+done:
+    for (int i = 0; i < n_env; i++) if (envs[i]) so_destroy(envs[i]);
+    free(envs);
+    free(obs);
+    return n;
 }

@@ -33,6 +33,7 @@ typedef struct {
     int32_t num_fruits;
     double  rew_fruit, rew_kill, rew_lose, rew_win, rew_time;
     double  max_episode_steps;
+    int32_t coop;             /* 1 = CoopSnakeEnv (coop_snake_env.py:14-22): any done ends it */
 } so_cfg;
 
 typedef struct {
@@ -45,7 +46,8 @@ so_env *so_create(const so_cfg *cfg, uint32_t seed);   /* np.random.seed(seed) +
 void    so_destroy(so_env *e);
 int64_t so_obs_size(const so_env *e);                  /* S*h*w*8*fs bytes */
 int     so_reset(so_env *e, uint8_t *obs);             /* snake_env.py:131-159 */
-/* snake_env.py:301-414. Returns 1 when all dones (info filled), 0 otherwise,
+/* snake_env.py:301-414. Returns 1 when the episode ended (_done_fn: all dones,
+ * or any done with coop; info filled), 0 otherwise,
  * -1 on an invalid action for an alive snake (the reference's KeyError). */
 int     so_step(so_env *e, const int32_t *actions, uint8_t *obs, double *rews,
                 uint8_t *dones, so_info *info);
@@ -58,6 +60,10 @@ void    so_get_snakes(const so_env *e, int32_t *out7xS);
  * grid (H*W, int32), snake k = coords[off[k]..off[k+1]) as (r,c) pairs, alive flags. */
 int     so_inject(so_env *e, const int32_t *grid, const int32_t *coords, const int32_t *off,
                   const uint8_t *alive, int64_t alive_snakes, int64_t episode_length);
+
+/* CPU-baseline driver: n_env envs (seeds seed..), `steps` steps each, random
+ * actions, all-done resets; returns env-steps run (-1 on error). */
+int64_t so_rollout(const so_cfg *cfg, int32_t n_env, uint32_t seed, int64_t steps, uint32_t act_seed);
 
 /* ---- RNG / tables (checked against tests/golden/rng.npz, candidates.npz) -- */
 void    so_rng_raw(uint32_t seed, int64_t n, uint32_t *out);

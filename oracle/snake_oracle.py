@@ -23,7 +23,8 @@ class SoCfg(ctypes.Structure):
                 ('observer', ctypes.c_int32), ('num_fruits', ctypes.c_int32),
                 ('rew_fruit', ctypes.c_double), ('rew_kill', ctypes.c_double),
                 ('rew_lose', ctypes.c_double), ('rew_win', ctypes.c_double),
-                ('rew_time', ctypes.c_double), ('max_episode_steps', ctypes.c_double)]
+                ('rew_time', ctypes.c_double), ('max_episode_steps', ctypes.c_double),
+                ('coop', ctypes.c_int32)]
 
 
 class SoInfo(ctypes.Structure):
@@ -65,6 +66,9 @@ def lib():
                                      ctypes.POINTER(ctypes.c_uint32)]
         L.so_rng_permutation.argtypes = [ctypes.c_uint32, ctypes.c_int64, P,
                                          ctypes.POINTER(ctypes.c_uint32)]
+        L.so_rollout.restype = ctypes.c_int64
+        L.so_rollout.argtypes = [ctypes.POINTER(SoCfg), ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64,
+                                 ctypes.c_uint32]
         L.so_candidates.restype = ctypes.c_int64
         L.so_candidates.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P]
         _lib = L
@@ -77,13 +81,14 @@ def _ptr(a):
 
 def make_cfg(height=20, width=20, num_snakes=4, snake_length=3, vision_range=None,
              frame_stack=1, observer='snake', reward_dict=None, num_fruits=None,
-             max_episode_steps=1e4):
+             max_episode_steps=1e4, coop=False):
     r = dict(DEFAULT_REWARD if reward_dict is None else reward_dict)
     if num_fruits is None:
         num_fruits = int(round(num_snakes * 0.8))
     return SoCfg(height, width, num_snakes, snake_length, int(vision_range or 0), frame_stack,
                  1 if observer == 'human' else 0, num_fruits, float(r['fruit']), float(r['kill']),
-                 float(r['lose']), float(r['win']), float(r['time']), float(max_episode_steps))
+                 float(r['lose']), float(r['win']), float(r['time']), float(max_episode_steps),
+                1 if coop else 0)
 
 
 class OracleEnv:
@@ -164,6 +169,16 @@ class OracleEnv:
                              int(alive_snakes), int(episode_length))
         if rc != 0:
             raise ValueError('inject failed')
+
+
+def rollout(n_env, seed, steps, act_seed=12345, **cfg):
+    """so_rollout: n_env C envs x `steps` random-action steps with all-done resets;
+    returns the env-steps run (the CPU baseline's unit of work)."""
+    c = make_cfg(**cfg)
+    n = lib().so_rollout(ctypes.byref(c), int(n_env), int(seed) & 0xffffffff, int(steps), int(act_seed))
+    if n < 0:
+        raise ValueError('so_rollout failed')
+    return int(n)
 
 
 def rng_raw(seed, n):

@@ -41,6 +41,7 @@ OUT = os.path.dirname(HERE)
 sys.path[:0] = [os.path.join(HERE, 'gymstub'), '/root/reference/marlenv']
 
 from marlenv.envs.snake_env import SnakeEnv  # noqa: E402
+from marlenv.envs.coop_snake_env import CoopSnakeEnv  # noqa: E402
 from marlenv.core.snake import Snake  # noqa: E402
 from marlenv.core import grid_util  # noqa: E402
 
@@ -127,9 +128,9 @@ def greedy_actions(env, rs, eps):
     return acts
 
 
-def run_traj(name, T, seed, policy='random', eps=0.1, full_obs_every=0, **kw):
+def run_traj(name, T, seed, policy='random', eps=0.1, full_obs_every=0, coop=False, **kw):
     np.random.seed(seed)
-    env = SnakeEnv(**kw)
+    env = (CoopSnakeEnv if coop else SnakeEnv)(**kw)
     S = env.num_snakes
     n_act = len(env.action_dict)
     rs = np.random.RandomState(seed + 100003)
@@ -177,6 +178,8 @@ def run_traj(name, T, seed, policy='random', eps=0.1, full_obs_every=0, **kw):
                frame_stack=env.frame_stack, observer=env.observer,
                reward_dict=env.reward_dict, num_fruits=env.num_fruits,
                max_episode_steps=float(env.max_episode_steps))
+    if coop:
+        cfg['coop'] = True
     f = lambda k, dt: np.array(rec[k], dtype=dt)  # noqa: E731
     np.savez_compressed(
         os.path.join(OUT, f'traj_{name}.npz'),
@@ -203,6 +206,20 @@ def run_traj(name, T, seed, policy='random', eps=0.1, full_obs_every=0, **kw):
 CUSTOM_REW = {'fruit': 1.0, 'kill': 2.0, 'lose': 3.0, 'win': 4.0, 'time': 0.1}  # test_snake.py:14-20
 KILL_REW = {'fruit': 1.0, 'kill': 1.0, 'lose': -1.0, 'win': 5.0, 'time': -0.01}
 SMALL_REW = {'fruit': 10.0, 'kill': 1.5, 'lose': -0.5, 'win': 2.0, 'time': -0.001}
+
+
+def make_coop_trajs():
+    # SnakeCoop-v1 (coop_snake_env.py:14-22): any done ends the episode, every
+    # done is then True; the statistics are masked with the per-snake dones
+    # before the override (snake_env.py:385-389), ranks come from any-done
+    run_traj('coop_vr5_s4', 500, 12, coop=True, height=20, width=20, num_snakes=4,
+             vision_range=5, full_obs_every=83)
+    run_traj('coop_trunc_s3', 300, 13, coop=True, height=10, width=10, num_snakes=3,
+             max_episode_steps=9, policy='greedy', eps=0.1, reward_dict=KILL_REW,
+             full_obs_every=47)
+    run_traj('coop_greedy_s2', 800, 14, coop=True, height=12, width=12, num_snakes=2,
+             snake_length=2, policy='greedy', eps=0.05, frame_stack=2, vision_range=3,
+             reward_dict=SMALL_REW, full_obs_every=157)
 
 
 def make_trajs():
@@ -381,3 +398,5 @@ if __name__ == '__main__':
         make_crafted()
     if 'traj' in which:
         make_trajs()
+    if 'traj' in which or 'coop' in which:
+        make_coop_trajs()

@@ -47,4 +47,4 @@ def env_kwargs(cfg):
                 snake_length=cfg['snake_length'], vision_range=cfg['vision_range'],
                 frame_stack=cfg['frame_stack'], observer=cfg['observer'],
                 reward_dict=cfg['reward_dict'], num_fruits=cfg['num_fruits'],
-                max_episode_steps=cfg['max_episode_steps'])
+                max_episode_steps=cfg['max_episode_steps'], **({'coop': True} if cfg.get('coop') else {}))

@@ -52,7 +52,7 @@ def test_plan_sizes(native):
     assert lay.n_cand == 3464 and lay.jscratch == 0
     assert lay.grid_stride == 400 and lay.ring_cap == 512
     assert lay.spawn == 65536 * 656 * 4                        # spawn-ahead records
-    assert lay.resetq == (2 * 64 * (4096 // 64) * 16 + 2 * 160) * 4   # two queues + counters
+    assert lay.resetq == (2 * 64 * (4096 // 64) * 16 + 160) * 4   # two queues + counters
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
     assert lay.obs_c == 32 and lay.obs == 8192 * 8 * 11 * 11 * 32
@@ -69,6 +69,8 @@ def test_plan_sizes(native):
     (dict(snake_length=1), 'snake_length'), (dict(height=2), 'height'),
     (dict(num_fruits=0), 'num_fruits'), (dict(frame_stack=0), 'frame_stack'),
     (dict(height=5, width=5, num_snakes=4, snake_length=3), 'too small'),
+    # 61 interior cells for 60 snake cells: ~1e-5 of the spawn draws are disjoint
+    (dict(height=3, width=63, num_snakes=4, snake_length=15), 'too crowded'),
 ])
 def test_plan_rejects(native, kw, msg):
     c = cfg(native, **kw)

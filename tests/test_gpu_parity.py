@@ -30,10 +30,12 @@ def _np(x):
 def test_compat_env_replays_golden(name):
     """make_snake(num_envs=1)-style SnakeEnv following numpy's global RNG, exactly
     as the reference does: np.random.seed(seed); env.reset(); env.step(...)."""
+    from marlenv.envs.coop_snake_env import CoopSnakeEnv
     from marlenv.envs.snake_env import SnakeEnv
     t = G.load_traj(name)
     np.random.seed(t['seed'])
-    env = SnakeEnv(**G.env_kwargs(t['config']))
+    kw = G.env_kwargs(t['config'])
+    env = (CoopSnakeEnv if kw.pop('coop', False) else SnakeEnv)(**kw)
     obs = env.reset()
     np.testing.assert_array_equal(obs, t['obs0'])
     n_reset = n_info = 0
@@ -131,6 +133,10 @@ BATCH_CASES = {
                                                                'win': 5.0, 'time': -0.01}), 4, 64, 300),
     'single_s1': (dict(height=10, width=10, vision_range=4, num_fruits=4), 1, 64, 300),
     'trunc_s2': (dict(height=12, width=12, max_episode_steps=7), 2, 64, 100),
+    # SnakeCoop-v1 (coop_snake_env.py:14-22): any-done episodes, truncation with coop
+    'coop_vr5_s4': (dict(height=20, width=20, vision_range=5, coop=True), 4, 96, 300),
+    'coop_trunc_s3_fs2': (dict(height=10, width=10, vision_range=2, frame_stack=2, coop=True,
+                               max_episode_steps=6), 3, 64, 150),
     's16': (dict(height=24, width=24, snake_length=2, vision_range=3), 16, 16, 200),
     # spawn-ahead for every env (include/snake_env.h): nearly every reset starts
     # from a ready record, partial records carry retries across steps
@@ -308,8 +314,18 @@ def test_invalid_actions():
     env.step([0, 0])
     v = SnakeVecEnv(4, num_snakes=2, seed=1)
     v.reset()
-    _, _, _, info = v.step(torch.tensor([[0, 0], [0, 7], [1, 2], [-1, 0]]))
+    g0 = _np(v.grids())
+    _, rew, done, info = v.step(torch.tensor([[0, 0], [0, 7], [1, 2], [-1, 0]]))
     assert _np(info['error']).tolist() == [0, 1, 0, 1]
+    # rejected envs: untouched, reward 0 and done False (defined outputs, not garbage)
+    rew, done = _np(rew), _np(done)
+    assert rew[[1, 3]].tobytes() == np.zeros((2, 2)).tobytes() and not done[[1, 3]].any()
+    np.testing.assert_array_equal(_np(v.grids())[[1, 3]], g0[[1, 3]])
+    ed = _np(info['episode_done'])
+    assert not ed[[1, 3]].any()
+    # the episode summary is zero wherever the episode did not end
+    for k in ('rank', 'episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills'):
+        assert not _np(info[k])[~ed].any(), k
     vs = SnakeVecEnv(2, num_snakes=2, seed=1, strict=True)
     vs.reset()
     with pytest.raises(KeyError):
@@ -377,3 +393,79 @@ def test_compat_render_modes(tmp_path):
     assert len(env.frame_buffer) == 3 and env.frame_buffer[0].size == (300, 300)
     fp = env.save_gif(str(tmp_path / 'play.gif'))
     assert (tmp_path / 'play.gif').stat().st_size > 0 and fp.endswith('play.gif')
+
+
+def test_info_zero_where_episode_continues():
+    """rank / episode_* are the episode summary where episode_done, zeros elsewhere."""
+    from marlenv import SnakeVecEnv
+    N, S = 512, 4
+    v = SnakeVecEnv(N, num_snakes=S, seed=2, height=10, width=10)
+    v.reset()
+    g = torch.Generator(device='cuda').manual_seed(5)
+    ended = 0
+    for t in range(60):
+        a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        _, _, _, info = v.step(a)
+        ed = info['episode_done']
+        ended += int(ed.sum())
+        assert not bool(info['rank'][~ed].any())
+        assert bool((info['rank'][ed] >= 1).all())
+        for k in ('episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills'):
+            assert not bool(info[k][~ed].any()), k
+    assert ended > 0
+
+
+@pytest.mark.parametrize('kw,S', [(dict(height=20, width=20, vision_range=5), 4),
+                                  (dict(height=12, width=12, frame_stack=3, vision_range=3, coop=True), 3),
+                                  (dict(height=44, width=44, vision_range=4, spawn_ahead=4), 4)])
+def test_snapshot_restore_roundtrip(kw, S):
+    """state_dict() mid-episode -> K steps -> load_state_dict() -> the same K steps
+    reproduce bit-identically, in the same env and in a fresh one (and from a
+    CPU copy, the torch.save path)."""
+    from marlenv import SnakeVecEnv
+    N, K = 256, 40
+    v = SnakeVecEnv(N, num_snakes=S, seed=31, **kw)
+    v.reset()
+    g = torch.Generator(device='cuda').manual_seed(8)
+    acts = torch.randint(0, 3, (60 + K, N, S), generator=g, device='cuda', dtype=torch.int8)
+    for t in range(60):
+        v.step(acts[t])
+    snap = v.state_dict()
+    snap_cpu = v.state_dict(device='cpu')
+
+    def roll(env):
+        outs = []
+        for t in range(60, 60 + K):
+            o, r, d, i = env.step(acts[t])
+            outs.append((o.clone(), r.clone(), d.clone(), i['episode_done'].clone(), env.grids().clone()))
+        return outs
+
+    ref = roll(v)
+    v.load_state_dict(snap)
+    again = roll(v)
+    fresh = SnakeVecEnv(N, num_snakes=S, seed=999, **kw)     # other seed: everything comes from the snapshot
+    fresh.load_state_dict(snap_cpu)
+    other = roll(fresh)
+    for t, (a, b, c) in enumerate(zip(ref, again, other)):
+        for x, y, z in zip(a, b, c):
+            assert torch.equal(x, y) and torch.equal(x, z), f'step {t}'
+    bad = SnakeVecEnv(N // 2, num_snakes=S, seed=31, **kw)
+    with pytest.raises(ValueError):
+        bad.load_state_dict(snap)
+
+
+def test_vec_env_on_non_current_device():
+    """A SnakeVecEnv on cuda:1 launches on its own device whatever device is current."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip('needs two GPUs')
+    from marlenv import SnakeVecEnv
+    torch.cuda.set_device(0)
+    a = SnakeVecEnv(64, num_snakes=4, seed=4, device='cuda:1', vision_range=5)
+    b = SnakeVecEnv(64, num_snakes=4, seed=4, device='cuda:0', vision_range=5)
+    assert torch.equal(a.reset().cpu(), b.reset().cpu())
+    g = torch.Generator().manual_seed(0)
+    for t in range(50):
+        act = torch.randint(0, 3, (64, 4), generator=g, dtype=torch.int8)
+        oa, ra, _, _ = a.step(act)
+        ob, rb, _, _ = b.step(act)
+        assert torch.equal(oa.cpu(), ob.cpu()) and torch.equal(ra.cpu(), rb.cpu())
