@@ -269,7 +269,8 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->jscratch = (round_up(2 * o->n_cand, 16) <= kJarrLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     o->spawn = N * kSpawnStride * 4;
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
-        // kQShards) with room for every env of its blocks, + two parities of counters
+        // kQShards) with room for every env of its blocks, + the step's counters
+        // (kQCount, each in its own line)
         const int64_t E = kWave / (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
         const int64_t blocks = (N + E - 1) / E;
         const int64_t cap = (blocks + kQShards - 1) / kQShards * E;

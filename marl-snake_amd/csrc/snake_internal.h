@@ -19,9 +19,18 @@ constexpr int kStageMax = 8192;     // bytes of staged observation per encode gr
 constexpr int kSpawnStride = 656;   // u32 words per spawn-ahead record: key, pos, poses
 constexpr int kSpawnPos = 624;      // record word: MT position after the recorded attempts
 constexpr int kSpawnSel = 625;      // record words [625, 625 + S): spawn-pose indices
-constexpr int kQCounters = 160;     // queue counters: 64 reset, 64 spawn, claim, worker exits
-constexpr int kQClaim = 128;        // counter word: next job index claimed by a free worker
-constexpr int kQExit = 129;         // counter word: k_autoreset workers finished
+// Queue counters (zero between steps). Every counter sits in a line of its own
+// (kQSpread words apart): same-line device-scope atomics from thousands of
+// waves serialise at the memory side.
+#ifndef SNAKE_QSPREAD
+#define SNAKE_QSPREAD 32
+#endif
+constexpr int kQSpread = SNAKE_QSPREAD;
+constexpr int kClaimShards = 16;    // claim counters: worker w claims on shard w % 16
+constexpr int kQClaim = 2 * kQShards;                 // counter index of claim shard 0
+constexpr int kQDone = kQClaim + kClaimShards;        // counter index: claim shards drained
+constexpr int kQCount = kQDone + 1;                   // counters
+constexpr int kQCounters = kQCount * kQSpread;        // words
 
 // env record words
 enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, ENV_FAIL = 5 };

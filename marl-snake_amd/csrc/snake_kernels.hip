@@ -990,7 +990,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && ep_end) : 0ull;
     const int shard = blockIdx.x % kQShards;
     int qbase = 0;
-    if (qm && lane == 0) qbase = atomicAdd(&qcnt[shard], __popcll(qm));
+    if (qm && lane == 0) qbase = atomicAdd(&qcnt[shard * kQSpread], __popcll(qm));
 
     // rewards, fp64 in the reference order (:354-370)
     const bool counted = death || alive;   // not previously dead
@@ -1165,7 +1165,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
                          __popc(am) <= c.spawn_thr;
     const unsigned long long pm = __ballot(spawn_q && k == 0);
     int pbase = 0;
-    if (pm && lane == 0) pbase = atomicAdd(&qcnt[kQShards + shard], __popcll(pm));
+    if (pm && lane == 0) pbase = atomicAdd(&qcnt[(kQShards + shard) * kQSpread], __popcll(pm));
 
     LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
@@ -1282,16 +1282,19 @@ __global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_stat
     // the shard counts of both queues, prefix-summed: queue index idx lives in
     // the shard whose [excl, incl) holds it
     int *qc = st.resetq + 2 * kQShards * c.q_cap;
-    const int cnt = qc[lane], pcnt = qc[kQShards + lane];
+    const int cnt = qc[lane * kQSpread], pcnt = qc[(kQShards + lane) * kQSpread];
     const int incl = wave_scan(cnt, lane), excl = incl - cnt;
     const int pincl = wave_scan(pcnt, lane), pexcl = pincl - pcnt;
     const int R = bcast(incl, kWave - 1), P = bcast(pincl, kWave - 1);
     if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
     // job idx < R: the step's resets (high priority, the critical path); idx >= R:
     // spawn-ahead jobs. A worker's first job is its block index, the next ones
-    // are claimed from the step's counter once it is free (a slow reset never
-    // holds up a job another worker could take).
-    for (int idx = blockIdx.x; idx < R + P;) {
+    // are claimed once it is free (a slow reset never holds up a job another
+    // worker could take): worker w claims on shard x = w % kClaimShards, whose
+    // n-th claim is job G + x + kClaimShards * n.
+    const int G = (int)gridDim.x, x = blockIdx.x % kClaimShards;
+    int idx = blockIdx.x, nx = 0;
+    for (;;) {
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
             const int sh = __ffsll((long long)__ballot(idx >= excl && idx < incl)) - 1;
@@ -1303,7 +1306,7 @@ __global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_stat
             if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
             else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
             if (idx < 128) OBSPROF(128 + idx, lane);
-        } else {
+        } else if (idx < R + P) {
             if (c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
             else if (c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(2);
@@ -1316,17 +1319,26 @@ __global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_stat
             else do_spawn<MS, false>(c, st, e, lds, blockIdx.x, lane);
             if (j < 128) OBSPROF(640 + j, lane);
         }
-        int nx = 0;
-        if (lane == 0) nx = atomicAdd(&qc[kQClaim], 1);
-        idx = (int)gridDim.x + bcast(nx, 0);
+        int v = 0;
+        if (lane == 0) v = atomicAdd(&qc[(kQClaim + x) * kQSpread], 1);
+        nx = bcast(v, 0);
+        idx = G + x + kClaimShards * nx;
+        if (idx >= R + P) break;
     }
-    // the last worker to finish re-zeroes the step's counters for the next step
-    // (every worker has read its counts and made its last claim before its exit
-    // count: the device state needs no host-side step parity)
-    int last = 0;
-    if (lane == 0) last = atomicAdd(&qc[kQExit], 1) == (int)gridDim.x - 1;
-    if (bcast(last, 0))
-        for (int q = lane; q < kQCounters; q += kWave) qc[q] = 0;
+    // Every worker ends with exactly one failing claim, so the shard's claims
+    // number its jobs + its workers, and the worker whose failing claim is the
+    // shard's last finishes the shard. The last shard to finish re-zeroes the
+    // step's counters for the next step: every worker has read its counts and
+    // made its last claim by then (no host-side step parity, one extra atomic
+    // per shard).
+    const int jobs_x = R + P > G + x ? (R + P - G - x + kClaimShards - 1) / kClaimShards : 0;
+    const int workers_x = (G - x + kClaimShards - 1) / kClaimShards;
+    if (nx == jobs_x + workers_x - 1) {
+        int d = 0;
+        if (lane == 0) d = atomicAdd(&qc[kQDone * kQSpread], 1);
+        if (bcast(d, 0) == min(G, kClaimShards) - 1)
+            for (int q = lane; q < kQCount; q += kWave) qc[q * kQSpread] = 0;
+    }
 }
 
 __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state st, const snake_out o)

@@ -12,10 +12,10 @@ for spec in "$@"; do
     if [[ $spec == *@* ]]; then
         tag=${spec%@*}; rev=${spec#*@}
         src=$OUT/src_$tag; mkdir -p "$src/csrc" "$src/include"
-        for f in snake_kernels.hip snake_capi.cpp snake_internal.h; do
+        for f in snake_kernels.hip snake_capi.cpp snake_internal.h dqn_kernels.hip; do
             git -C "$ROOT" show "$rev:marl-snake_amd/csrc/$f" > "$src/csrc/$f"
         done
-        git -C "$ROOT" show "$rev:include/snake_env.h" > "$src/include/snake_env.h"
+        git -C "$ROOT" show "$rev:include/snake_env.h" | sed "s/define SNAKE_ABI_VERSION .*/define SNAKE_ABI_VERSION ${ABI:-8}/" > "$src/include/snake_env.h"
         sed -i 's#"../../include/snake_env.h"#"../include/snake_env.h"#' "$src/csrc/snake_internal.h"
         extra=""; dir=$src/csrc
     else
