@@ -17,6 +17,11 @@ reset() reproduces the reference trajectory bit for bit, and user code that
 interleaves its own np.random calls sees the same stream it would with the
 reference. (rng='own' keeps a private per-env stream seeded with ``seed``.)
 
+Transfers: one pinned host->device copy and one device->host copy per call
+(_setup_io); code that writes this env's device state directly (the vector
+env's set_mt_state/inject on env._vec) calls env._fetch() afterwards so the
+host mirror of the key and env record is current.
+
 Deviation: on an invalid action the reference raises KeyError after having
 already turned the lower-index snakes; here KeyError is raised with the env
 untouched.
@@ -73,37 +78,105 @@ class SnakeEnv:
             raise ValueError("rng must be 'global' or 'own'")
         self._rng = rng
         self.np_random = None
-        torch = _torch()
-        self._pin = torch.empty(0)
+        self._setup_io()
 
-    # ------------------------------------------------------------- RNG sync
-    def _push_rng(self):
+    # ------------------------------------------------------- packed transfers
+    def _setup_io(self):
+        """One device buffer holds everything a step moves between host and
+        device: [MT key | env record | actions | obs | rew | done | ep_done |
+        rank | ep_stats | err]. The env's key and env-record state tensors are
+        re-pointed into it, so a step is ONE pinned host->device copy (the
+        global numpy MT19937 state, the env record, the actions), the launches,
+        and ONE device->host copy (outputs + the advanced key) -- instead of a
+        624-word push, scalar writes, a gather and three read-backs."""
+        torch = _torch()
+        v, S = self._vec, self.num_snakes
+        dev = v.device
+        obs_bytes = int(np.prod(v.obs_shape))
+        sizes = [('env', 32), ('mt', 624 * 4), ('act', S), ('obs', obs_bytes), ('rew', 8 * S), ('done', S),
+                 ('ep_done', 1), ('rank', 4 * S), ('ep_stats', 32 * S), ('err', 4)]
+        off, o = {}, 0
+        for name, n in sizes:
+            off[name] = (o, n)
+            o = (o + n + 15) // 16 * 16
+        # bytes [12, obs) go host -> device: env words 3.. (MT position, spawn
+        # status, failure flag), the key, the actions; words 0-2 (alive, episode
+        # length, ring slot) are only ever written on the device
+        self._io_in = off['obs'][0]
+        self._io_bytes = o
+        buf = torch.zeros(o, dtype=torch.uint8, device=dev)
+        buf[off['mt'][0]:off['mt'][0] + 2496].copy_(v.mt.view(torch.uint8)[:2496])
+        buf[off['env'][0]:off['env'][0] + 32].copy_(v.env_rec.view(torch.uint8)[:32])
+        view = lambda name, dt: buf[off[name][0]:off[name][0] + off[name][1]].view(dt)  # noqa: E731
+        v.mt = view('mt', torch.int32)
+        v.env_rec = view('env', torch.int32)
+        st = v._state
+        st.mt = v.mt.data_ptr()
+        st.env = v.env_rec.data_ptr()
+        self._dev = buf
+        self._act_dev = view('act', torch.int8)
+        self._obs_dev = view('obs', torch.uint8).view((1,) + v.obs_shape)
+        from .._native import SnakeOut
+        self._so = SnakeOut(*(buf.data_ptr() + off[k][0] for k in ('obs', 'rew', 'done', 'ep_done', 'rank',
+                                                                    'ep_stats', 'err')))
+        self._hin = torch.empty(self._io_in, dtype=torch.uint8, pin_memory=True)
+        self._hout = torch.empty(o, dtype=torch.uint8, pin_memory=True)
+        hin, hout = self._hin.numpy(), self._hout.numpy()
+        self._in_key = hin[off['mt'][0]:off['mt'][0] + 2496].view(np.uint32)
+        self._in_env = hin[off['env'][0]:off['env'][0] + 32].view(np.int32)
+        self._in_act = hin[off['act'][0]:off['act'][0] + S].view(np.int8)
+        hv = lambda name, dt: hout[off[name][0]:off[name][0] + off[name][1]].view(dt)  # noqa: E731
+        self._out = {k: hv(k, dt) for k, dt in (('mt', np.uint32), ('env', np.int32), ('obs', np.uint8),
+                                                 ('rew', np.float64), ('done', np.uint8), ('ep_done', np.uint8),
+                                                 ('rank', np.int32), ('ep_stats', np.float64), ('err', np.int32))}
+        self._fetch()                                   # host mirror of the key and env record
+
+    def _fetch(self, upto=None):
+        torch = _torch()
+        n = self._io_bytes if upto is None else upto
+        self._hout[:n].copy_(self._dev[:n], non_blocking=True)
+        torch.cuda.current_stream(self._vec.device).synchronize()
+
+    def _stage_in(self, acts=None):
+        """Host side of the push: the key (numpy's global MT19937, or the env's
+        own), the env record as last fetched (MT position from numpy's state, the
+        spawn-ahead record voided as set_mt_state does), the actions."""
+        out = self._out
+        self._in_env[:] = out['env']
+        if self._rng == 'global':
+            st = np.random.get_state(legacy=True)
+            self._in_key[:] = np.asarray(st[1], dtype=np.uint32)
+            self._in_env[3] = int(st[2])
+            self._in_env[4] = 0
+        else:
+            self._in_key[:] = out['mt']
+        if acts is not None:
+            self._in_act[:] = acts
+        self._dev[12:self._io_in].copy_(self._hin[12:], non_blocking=True)
+
+    def _publish_rng(self):
         if self._rng != 'global':
             return
-        torch = _torch()
         st = np.random.get_state(legacy=True)
-        key = np.ascontiguousarray(np.asarray(st[1], dtype=np.uint32)).view(np.int32)
-        self._vec.set_mt_state(0, torch.from_numpy(key), int(st[2]))
-
-    def _pull_rng(self):
-        if self._rng != 'global':
-            return
-        mt, pos = self._vec.mt_state()
-        key = mt[0].cpu().numpy().view(np.uint32).copy()
-        p = int(pos[0].item())
-        st = np.random.get_state(legacy=True)
-        np.random.set_state((st[0], key, p, st[3], st[4]))
+        np.random.set_state((st[0], self._out['mt'].copy(), int(self._out['env'][3]), st[3], st[4]))
 
     # -------------------------------------------------------------- the API
     def reset(self):
-        self._push_rng()
-        obs = self._vec.reset()
-        out = obs[0].cpu().numpy()
-        self._pull_rng()
-        if int(self._vec.spawn_failures()[0]):
+        import ctypes
+        torch = _torch()
+        v = self._vec
+        self._stage_in()
+        with torch.cuda.device(v.device):
+            from .._native import check
+            check(v._L.snake_reset(ctypes.byref(v.cfg), ctypes.byref(v._state), 1, None,
+                                   ctypes.byref(self._so), v._stream()))
+        v._reset_done = True
+        self._fetch()
+        self._publish_rng()
+        if int(self._out['env'][5]):
             raise RuntimeError('reset gave up after 2^16 spawn permutations without disjoint snakes')
         self.frame_buffer = []
-        return np.array(out, dtype=np.uint8)
+        return self._out['obs'].reshape(v.obs_shape).copy()
 
     def seed(self, seed=42):
         # snake_env.py:161-163 only seeds an unused self.np_random
@@ -111,6 +184,7 @@ class SnakeEnv:
         return [seed]
 
     def step(self, actions):
+        import ctypes
         if isinstance(actions, int):
             actions = [actions]
         assert len(actions) == self.num_snakes
@@ -123,38 +197,29 @@ class SnakeEnv:
             acts.append(int(a))
         if self.observer == 'human':
             acts = [a if 0 <= a <= 4 else 0 for a in acts]  # non-matching actions keep the heading
-        self._push_rng()
-        obs, rew, done, info = self._vec.step(np.array(acts, np.int64).reshape(1, -1))
-        torch = _torch()
-        packed = [obs[0].reshape(-1), rew[0].view(torch.uint8), done[0].view(torch.uint8),
-                  info['episode_done'].view(torch.uint8), info['rank'][0].view(torch.uint8),
-                  info['episode_scores'][0].contiguous().view(torch.uint8),
-                  info['episode_steps'][0].contiguous().view(torch.uint8),
-                  info['episode_fruits'][0].contiguous().view(torch.uint8),
-                  info['episode_kills'][0].contiguous().view(torch.uint8),
-                  info['error'].view(torch.uint8)]
-        host = torch.cat(packed).cpu().numpy()
-        self._pull_rng()
-        S = self.num_snakes
-        o = 0
-        n = obs[0].numel()
-        obs_np = host[o:o + n].reshape(self._vec.obs_shape).copy(); o += n
-        rews = host[o:o + 8 * S].view(np.float64); o += 8 * S
-        dones = host[o:o + S].astype(bool); o += S
-        ep_done = bool(host[o]); o += 1
-        rank = host[o:o + 4 * S].view(np.int32); o += 4 * S
-        stats = []
-        for _ in range(4):
-            stats.append(host[o:o + 8 * S].view(np.float64).copy()); o += 8 * S
-        err = int(host[o:o + 4].view(np.int32)[0])
-        if err:
+        v = self._vec
+        if not v._reset_done:
+            raise RuntimeError('call reset() before step()')
+        acts = np.clip(np.asarray(acts, np.int64), -128, 127).astype(np.int8)
+        self._stage_in(acts)
+        from .._native import check
+        check(v._L.snake_step(ctypes.byref(v.cfg), ctypes.byref(v._state), 1,
+                              ctypes.c_void_p(self._act_dev.data_ptr()), ctypes.byref(self._so), v._stream()))
+        self._fetch()
+        out = self._out
+        if int(out['err'][0]) == 1:
+            # the env was left untouched on the device; numpy's stream was not advanced
             raise KeyError('invalid action for an alive snake (action_angle_dict lookup)')
+        self._publish_rng()
+        S = self.num_snakes
         info_out = {}
-        if ep_done:
-            info_out = {'rank': [np.int64(r) for r in rank],
-                        'episode_scores': stats[0], 'episode_steps': stats[1],
-                        'episode_fruits': stats[2], 'episode_kills': stats[3]}
-        return obs_np, [float(r) for r in rews], [bool(d) for d in dones], info_out
+        if out['ep_done'][0]:
+            es = out['ep_stats'].reshape(4, S)
+            info_out = {'rank': [np.int64(r) for r in out['rank']],
+                        'episode_scores': es[0].copy(), 'episode_steps': es[1].copy(),
+                        'episode_fruits': es[2].copy(), 'episode_kills': es[3].copy()}
+        return (out['obs'].reshape(v.obs_shape).copy(), [float(r) for r in out['rew']],
+                [bool(d) for d in out['done']], info_out)
 
     def _done_fn(self, dones):
         return all(dones)

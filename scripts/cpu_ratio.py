@@ -44,6 +44,32 @@ def ref_rollout(kw, seconds, n_env=16, S=4):
     return steps / (time.perf_counter() - t0)
 
 
+def ref_single(kw, seconds, S=4):
+    """One reference env the way train_dqn.py drives it (reset when all done):
+    ms per step() and per reset()."""
+    from marlenv.envs.snake_env import SnakeEnv
+    np.random.seed(0)
+    e = SnakeEnv(num_snakes=S, **kw)
+    e.reset()
+    rs = np.random.RandomState(1)
+    st = rt = 0.0
+    n = nr = 0
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        a = [int(x) for x in rs.randint(0, 3, S)]
+        t0 = time.perf_counter()
+        _, _, d, _ = e.step(a)
+        st += time.perf_counter() - t0
+        n += 1
+        if all(d):
+            t0 = time.perf_counter()
+            e.reset()
+            rt += time.perf_counter() - t0
+            nr += 1
+    return {'step_ms': round(st / n * 1e3, 4), 'reset_ms': round(rt / max(nr, 1) * 1e3, 4), 'steps': n,
+            'resets': nr}
+
+
 def port_rollout(kw, seconds, n_env=16, S=4):
     """oracle/snake_oracle.c's so_rollout (no Python in the loop)."""
     from oracle.snake_oracle import rollout
@@ -65,6 +91,9 @@ def main():
                      'port_env_steps_per_s_1core': round(port, 1),
                      'port_over_reference': round(port / ref, 2)}
         print(name, out[name], flush=True)
+    # the num_envs=1 path of train_dqn.py's Config (20x20, 4 snakes, length 5, full map)
+    out['compat_train_dqn_reference'] = ref_single(dict(height=20, width=20, snake_length=5), seconds)
+    print('compat', out['compat_train_dqn_reference'], flush=True)
     out['note'] = ('one core each, 16 envs round-robin, random actions, all-done resets included; '
                    'reference = /root/reference SnakeEnv under the offline gym stub '
                    '(tests/golden/gen/gymstub), port = oracle/snake_oracle.c so_rollout (C loop, xorshift actions)')
