@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 8
+#define SNAKE_ABI_VERSION 9
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -59,8 +59,10 @@ typedef struct {
 /* Byte sizes of every caller-allocated buffer for num_envs envs (snake_plan). */
 typedef struct {
     int64_t grid;       /* uint8  [N][fs][grid_stride]   grid ring (newest = env[2]) */
-    int64_t snake;      /* int32  [N][S][4]              packed snake records */
-    int64_t body;       /* uint8  [N][S][ring_cap]       direction deques (rings) */
+    int64_t snake;      /* int32  [N][S][4]              packed snake records: head/tail cells; heading,
+                                                         alive, pending ring-word directions; ring head and
+                                                         length; tail-direction queue (see k_logic) */
+    int64_t body;       /* uint8  [N][S][ring_cap]       direction deques (rings), ring_cap >= 16 */
     int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos,
                                                          spawn-ahead status (0 none, 1 partial, 2 ready),
                                                          spawn failure (1: the last reset gave up, below) */

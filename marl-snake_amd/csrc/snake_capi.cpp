@@ -251,7 +251,8 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     const int oh = c->vision_range ? 2 * c->vision_range + 1 : c->height;
     const int ow = c->vision_range ? 2 * c->vision_range + 1 : c->width;
     o->grid_stride = (int32_t)round_up(HW, 16);
-    o->ring_cap = pow2_at_least((c->height - 2) * (c->width - 2));
+    // >= 16: the step reads the rings as aligned 8-byte chunks and writes 4-byte words
+    o->ring_cap = std::max(16, pow2_at_least((c->height - 2) * (c->width - 2)));
     o->n_cand = cached_count(c->height, c->width, c->snake_length);
     o->obs_h = oh; o->obs_w = ow; o->obs_c = 8 * c->frame_stack;
     o->grid = N * fs * o->grid_stride;

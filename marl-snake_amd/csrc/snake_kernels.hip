@@ -774,7 +774,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
             rec.y = dir_of_diff(cell - nxt, W) | (1 << 8);
             rec.z = 0 | ((L - 1) << 16);
             // cached directions[-1] (the direction move() pops next)
-            rec.w = dir_of_diff(pretail - tailcell, W);
+            rec.w = dir_of_diff(pretail - tailcell, W) | (1 << 28);   // tail queue: directions[-1] only
             reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + sk] = rec;
             const int og = pack_origin(c, hr, hc);
             for (int f = 0; f < c.fs; f++) {
@@ -919,7 +919,15 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     int hr = rec.x & 255, hc = (rec.x >> 8) & 255, tr = (rec.x >> 16) & 255, tc = (rec.x >> 24) & 255;
     int dir = rec.y & 3, alive = (rec.y >> 8) & 1;
     int rh = rec.z & 0xffff, rl = (rec.z >> 16) & 0xffff;
-    const int tdir = rec.w;                   // cached directions[-1] (core/snake.py:103)
+    // Direction deque (body ring) traffic: the ring word holding the head is
+    // written once per 4 pushes (pending directions in rec.y bits 16-23, 2 bits
+    // per byte offset), and the tail end is read as aligned 8-byte chunks into a
+    // queue in rec.w (entry 0 = directions[-1], then directions[-2], ...; count
+    // in bits 28-31). One byte store and one line fetch per snake and step
+    // were the largest share of k_logic's traffic.
+    uint32_t tq = (uint32_t)rec.w;
+    const int tdir = (int)(tq & 3u);          // directions[-1] (core/snake.py:103)
+    int hbuf = (rec.y >> 16) & 255;
 
     // snake_env.py:318-330 heading + target cell per alive snake
     const bool mv0 = isn && alive;
@@ -1020,18 +1028,42 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     }
     wave_sync();
     uint8_t *ring = st.body + ((int64_t)e * S + k) * cap;
-    int nhr = hr, nhc = hc, ntr = tr, ntc = tc, ntdir = tdir;
+    int nhr = hr, nhc = hc, ntr = tr, ntc = tc;
     if (alive) {
         work[hr * W + hc] = (uint8_t)(C_BODY + 10 * k);
         nhr = hr + dir_dr(dir);
         nhc = hc + dir_dc(dir);
         rh = (rh - 1) & (cap - 1);                                   // directions.appendleft
-        ring[rh] = (uint8_t)dir;
+        const int ho = rh & 3;
+        hbuf = (hbuf & ~(3 << (2 * ho))) | (dir << (2 * ho));
+        if (ho == 0) {                                               // the head word is complete
+            *reinterpret_cast<uint32_t *>(ring + rh) = (uint32_t)(hbuf & 3) | ((uint32_t)(hbuf >> 2 & 3) << 8) |
+                                                       ((uint32_t)(hbuf >> 4 & 3) << 16) |
+                                                       ((uint32_t)(hbuf >> 6 & 3) << 24);
+            hbuf = 0;
+        }
         if (!eat) {                                                  // directions.pop()
             ntr = tr + dir_dr(tdir);
             ntc = tc + dir_dc(tdir);
-            // next directions[-1]; with one direction left it is the one just pushed
-            ntdir = (rl == 1) ? dir : ring[(rh + rl - 1) & (cap - 1)];
+            const uint32_t cnt = (tq >> 28) - 1u;
+            tq = ((tq & 0x0fffffffu) >> 2) | (cnt << 28);
+            if (cnt == 0u) {
+                // refill from the chunk holding the new directions[-1] (position t):
+                // t, t-1, .. down to the chunk start, but not below the head (the
+                // positions past it are free ring slots); pending head-word bytes
+                // come from hbuf
+                const int t = (rh + rl - 1) & (cap - 1), base = t & ~7;
+                const uint64_t q = *reinterpret_cast<const uint64_t *>(ring + base);
+                const int n = min(t - base + 1, ((t - rh) & (cap - 1)) + 1);
+                uint32_t nq = 0;
+                for (int j = 0; j < n; j++) {
+                    const int p = t - j;
+                    int d = (int)(q >> (8 * (p - base))) & 3;
+                    if (ho != 0 && (p >> 2) == (rh >> 2) && p >= rh) d = (hbuf >> (2 * (p & 3))) & 3;
+                    nq |= (uint32_t)d << (2 * j);
+                }
+                tq = nq | ((uint32_t)n << 28);
+            }
         } else {
             rl++;
         }
@@ -1053,6 +1085,11 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
             int d[16];
 #pragma unroll
             for (int t = 0; t < 16; t++) d[t] = (m0 + t < n) ? rk[(rh + m0 + t) & (cap - 1)] : 0;
+            if (m0 == 0 && (rh & 3) != 0) {                          // the pending head-word bytes
+#pragma unroll
+                for (int t = 0; t < 3; t++)
+                    if (t < 4 - (rh & 3)) d[t] = (hbuf >> (2 * ((rh & 3) + t))) & 3;
+            }
 #pragma unroll
             for (int t = 0; t < 16; t++) {
                 if (m0 + t < n) {
@@ -1231,9 +1268,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         st.ctr[((int64_t)e * fs + ncur) * S + k] = (uint16_t)((chr << 8) | chc);
         int4 nrec;
         nrec.x = nhr | (nhc << 8) | (ntr << 16) | (ntc << 24);
-        nrec.y = dir | (alive << 8);
+        nrec.y = dir | (alive << 8) | (hbuf << 16);
         nrec.z = rh | (rl << 16);
-        nrec.w = ntdir;
+        nrec.w = (int)tq;                 // entry 0 = the new directions[-1]
         reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + k] = nrec;
     }
     LSTAMP(47);

@@ -298,8 +298,9 @@ class SnakeVecEnv:
             body[k, :len(dirs)] = dirs
             (hr, hc), (tr, tc) = co[0], co[-1]
             x = hr | (hc << 8) | (tr << 16) | (tc << 24)
+            # rec.w: the tail queue (directions[-1], count 1), see k_logic
             rec[k] = [x - (1 << 32) if x >= (1 << 31) else x, dirs[0] | (int(bool(alive)) << 8),
-                      (len(co) - 1) << 16, dirs[-1]]
+                      (len(co) - 1) << 16, dirs[-1] | (1 << 28)]
         # crop centres of the refilled frames: the own HEAD cell (argmax of the own
         # head plane, snake_env.py:500-501), (0, 0) when there is none
         g2 = np.asarray(grid, np.int64).reshape(H, W)
