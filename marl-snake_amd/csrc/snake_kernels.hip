@@ -1241,7 +1241,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         es[2 * S + k] = ep_end ? s2 : 0.0; es[3 * S + k] = ep_end ? s3 : 0.0;
     }
     if (ep_end) s0 = s1 = s2 = s3 = 0.0;                           // _reset_epi_stats
-    if (live) { sp[k] = s0; sp[S + k] = s1; sp[2 * S + k] = s2; sp[3 * S + k] = s3; }
+    // a snake dead before this step keeps its statistics, record and (one frame)
+    // crop centre: no stores for it
+    if (live && (counted || ep_end)) { sp[k] = s0; sp[S + k] = s1; sp[2 * S + k] = s2; sp[3 * S + k] = s3; }
 
     LSTAMP(46);
     // commit the new frames into their ring slots; records; crop centres
@@ -1264,8 +1266,8 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         ner.x = alive_snakes; ner.y = eplen1; ner.z = ncur; ner.w = mtpos_new;
         *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = ner;
     }
-    if (live) {
-        st.ctr[((int64_t)e * fs + ncur) * S + k] = (uint16_t)((chr << 8) | chc);
+    if (live && (counted || fs > 1)) st.ctr[((int64_t)e * fs + ncur) * S + k] = (uint16_t)((chr << 8) | chc);
+    if (live && counted) {
         int4 nrec;
         nrec.x = nhr | (nhc << 8) | (ntr << 16) | (ntc << 24);
         nrec.y = dir | (alive << 8) | (hbuf << 16);
