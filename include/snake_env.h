@@ -63,7 +63,9 @@ typedef struct {
                                                          alive, pending ring-word directions; ring head and
                                                          length; tail-direction queue (see k_logic) */
     int64_t body;       /* uint8  [N][S][ring_cap]       direction deques (rings), ring_cap >= 16 */
-    int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos,
+    int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos
+                                                         (> 624: the key's twist is pending, position
+                                                         624 + j = word j of the next key),
                                                          spawn-ahead status (0 none, 1 partial, 2 ready),
                                                          spawn failure (1: the last reset gave up, below) */
     int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */

@@ -265,7 +265,7 @@ __device__ void mt_twist(WaveMT &m, int lane)
     }
 #pragma unroll
     for (int t = 0; t < 10; t++) m.w[t] = nw[t];
-    m.pos = 0;
+    m.pos -= kMtN;   // a pending twist: position 624 + j is word j of the new key
 }
 
 // One masked bounded draw: first raw r (in stream order) with (r & mask) <= rng.
@@ -1132,11 +1132,25 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         const uint32_t rng = (uint32_t)(Etot - 1), rmask = gen_mask(rng);
         // rng == 0 draws nothing (randint(0, 1) consumes no raw word)
         const bool draws = need && Etot > 0 && rng != 0;
-        const bool room = mtpos + G * kRespawnT <= kMtN;
+        // the next G * kRespawnT raw words of the stream; past the key's end they
+        // are words of the next key, computed from the old one (new[j] for
+        // j < 227 needs old[j], old[j+1] and old[j+397] only): the twist is left
+        // pending in the stored position (> 624), every MT consumer applies it
+        const bool room = mtpos + G * kRespawnT <= kMtN + 226;
+        const uint32_t *key = st.mt + (int64_t)e * kMtN;
         uint32_t accm = 0;
 #pragma unroll
         for (int t = 0; t < kRespawnT; t++) {
-            const uint32_t raw = (draws && room) ? st.mt[(int64_t)e * kMtN + mtpos + t * G + k] : 0u;
+            const int pw = mtpos + t * G + k;
+            uint32_t raw = 0u;
+            if (draws && room) {
+                if (pw < kMtN) {
+                    raw = key[pw];
+                } else {
+                    const int j = pw - kMtN;
+                    raw = mt_mix(key[j], key[j + 1], key[j + 397]);
+                }
+            }
             const uint32_t tv = temper(raw) & rmask;
             rawbuf[t * G + k] = tv;
             accm |= gbits(__ballot(draws && room && tv <= rng)) << (t * G);

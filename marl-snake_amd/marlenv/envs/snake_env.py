@@ -40,6 +40,22 @@ FEATURE_CHANNEL = 8     # envs/constants.py:2
 RGB_CHANNEL = 3         # envs/constants.py:1
 
 
+def _mt_twist(key):
+    """mt19937_gen on a uint32[624] key (numpy's generator), in three slices:
+    new[i] mixes old[i], old[i+1] and old[i+397] for i < 227, new[i-227] after,
+    and the last word wraps to new[0]."""
+    k = key.astype(np.uint32).copy()
+
+    def mix(cur, nxt, x):
+        y = (cur & np.uint32(0x80000000)) | (nxt & np.uint32(0x7fffffff))
+        return x ^ (y >> np.uint32(1)) ^ np.where(y & np.uint32(1), np.uint32(0x9908b0df), np.uint32(0))
+    k[0:227] = mix(k[0:227], k[1:228], k[397:624])
+    k[227:454] = mix(k[227:454], k[228:455], k[0:227])
+    k[454:623] = mix(k[454:623], k[455:624], k[227:396])
+    k[623] = mix(k[623:624], k[0:1], k[396:397])[0]
+    return k
+
+
 class SnakeEnv:
     default_action_dict = DEFAULT_ACTION_DICT
     action_angle_dict = ACTION_ANGLE_DICT
@@ -157,8 +173,11 @@ class SnakeEnv:
     def _publish_rng(self):
         if self._rng != 'global':
             return
+        key, pos = self._out['mt'].copy(), int(self._out['env'][3])
+        if pos > 624:          # the device left the key's twist pending (include/snake_env.h)
+            key, pos = _mt_twist(key), pos - 624
         st = np.random.get_state(legacy=True)
-        np.random.set_state((st[0], self._out['mt'].copy(), int(self._out['env'][3]), st[3], st[4]))
+        np.random.set_state((st[0], key, pos, st[3], st[4]))
 
     # -------------------------------------------------------------- the API
     def reset(self):

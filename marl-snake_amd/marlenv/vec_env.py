@@ -264,7 +264,9 @@ class SnakeVecEnv:
 
     def mt_state(self):
         """(N, 624) MT19937 keys (int32 view of uint32) and (N,) positions (read-only
-        use: writers go through set_mt_state)."""
+        use: writers go through set_mt_state). A position above 624 means the key's
+        twist is pending: position 624 + j is word j of the next key (numpy's
+        state is the twisted key at position - 624)."""
         return self.mt.view(self.num_envs, 624), self.env_rec.view(self.num_envs, 8)[:, 3]
 
     def set_mt_state(self, i, key, pos):
