@@ -49,7 +49,9 @@ typedef struct {
     int32_t coop;               /* 1 = SnakeCoop-v1: episode ends when ANY snake dies */
     int32_t autoreset;          /* 1 = reset an env inside snake_step when all its dones
                                    are True and return the reset obs (vector-env semantics,
-                                   wrappers.py:139-145); 0 = return the terminal obs */
+                                   wrappers.py:139-145); 0 = return the terminal obs;
+                                   2 = reset every env after every step (gym 0.23.1's
+                                   worker behind make_snake, wrappers.py:212) */
     int32_t spawn_ahead;        /* spawn-ahead threshold (snake_step): 0 = default (at most
                                    2 live snakes, every env under coop; the environment
                                    variable SNAKE_SPAWN_THR overrides), -1 = off, k >= 1 =

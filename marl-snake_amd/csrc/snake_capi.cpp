@@ -318,7 +318,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->H = c->height; k->W = c->width; k->HW = c->height * c->width;
     k->S = c->num_snakes; k->L = c->snake_length; k->vr = c->vision_range;
     k->fs = c->frame_stack; k->observer = c->observer; k->num_fruits = c->num_fruits;
-    k->coop = c->coop ? 1 : 0; k->autoreset = c->autoreset ? 1 : 0;
+    k->coop = c->coop ? 1 : 0; k->autoreset = c->autoreset == 2 ? 2 : (c->autoreset ? 1 : 0);
     k->oh = lay.obs_h; k->ow = lay.obs_w;
     k->units = k->S * k->oh * k->ow * k->fs;
     k->grid_stride = lay.grid_stride; k->ring_cap = lay.ring_cap; k->n_cand = (int)lay.n_cand;
@@ -378,7 +378,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     static const char *ev = getenv("SNAKE_SPAWN_THR");
     if (c->spawn_ahead != 0) k->spawn_thr = c->spawn_ahead < 0 ? -1 : c->spawn_ahead;
     else k->spawn_thr = ev ? atoi(ev) : (k->coop ? k->S : 2);
-    if (!k->autoreset) k->spawn_thr = -1;
+    if (k->autoreset != 1) k->spawn_thr = -1;   // (every-step resets: nothing to draw ahead)
     k->lds_obs_bytes = off;
     // the reset workers never use the encode staging buffer: the draw record
     // overlays it (the workers' LDS is what k_encode's waves share the CUs with)

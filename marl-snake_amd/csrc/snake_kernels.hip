@@ -995,7 +995,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const uint32_t all_m = (1u << S) - 1u;
     const bool ep_end = !bad && (c.coop ? (done_m != 0u) : (done_m == all_m));
     if (c.coop && ep_end) fd = 1;
-    const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && ep_end) : 0ull;
+    // (autoreset 2: every env, gym 0.23.1's reset after every step)
+    const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && !bad && (ep_end || c.autoreset == 2))
+                                              : 0ull;
     const int shard = blockIdx.x % kQShards;
     int qbase = 0;
     if (qm && lane == 0) qbase = atomicAdd(&qcnt[shard * kQSpread], __popcll(qm));
@@ -1683,6 +1685,14 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;
+    if (k.autoreset == 2) {   // every env resets: no encode, the resets write every obs
+        TimedLaunch t2("k_autoreset", sm);
+        if (k.S <= 4) hipLaunchKernelGGL(k_autoreset<4>, gr, block, k.lds_bytes, sm, k, st, o);
+        else if (k.S <= 8) hipLaunchKernelGGL(k_autoreset<8>, gr, block, k.lds_bytes, sm, k, st, o);
+        else hipLaunchKernelGGL(k_autoreset<16>, gr, block, k.lds_bytes, sm, k, st, o);
+        t2.close();
+        return check_launch("k_autoreset");
+    }
     if (!k.autoreset) {
         TimedLaunch t3("k_encode", sm);
         hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);

@@ -19,6 +19,18 @@ DEFAULT_ACTION_DICT = {'noop': 0, 'left': 1, 'right': 2, 'down': 3, 'up': 4}
 ACTION_ANGLE_DICT = {0: 0.0, 1: math.pi / 2.0, 2: -math.pi / 2.0}
 
 
+def autoreset_code(autoreset):
+    """True -> 1 (reset when all dones are True, wrappers.py:141-143), False -> 0,
+    'every_step' -> 2: gym 0.23.1's worker as make_snake's AsyncVectorEnv runs it
+    (`if done: reset` on the list of dones, always truthy: a reset after every
+    step)."""
+    if autoreset == 'every_step':
+        return 2
+    if isinstance(autoreset, str):
+        raise ValueError(f"autoreset must be True, False or 'every_step' (got {autoreset!r})")
+    return 1 if autoreset else 0
+
+
 def build_cfg(height=20, width=20, num_snakes=4, snake_length=3, vision_range=None,
               frame_stack=1, observer='snake', coop=False, autoreset=True, **kwargs):
     reward_dict = kwargs.pop('reward_dict', DEFAULT_REWARD_DICT)
@@ -35,7 +47,7 @@ def build_cfg(height=20, width=20, num_snakes=4, snake_length=3, vision_range=No
         int(frame_stack), 1 if observer == 'human' else 0, int(num_fruits),
         float(reward_dict['fruit']), float(reward_dict['kill']), float(reward_dict['lose']),
         float(reward_dict['win']), float(reward_dict['time']), float(max_episode_steps),
-        1 if coop else 0, 1 if autoreset else 0, spawn_ahead)
+        1 if coop else 0, autoreset_code(autoreset), spawn_ahead)
     meta = dict(height=int(height), width=int(width), num_snakes=int(num_snakes),
                 snake_length=int(snake_length), vision_range=vision_range,
                 frame_stack=int(frame_stack), observer=observer, reward_dict=reward_dict,

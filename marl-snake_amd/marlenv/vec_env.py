@@ -13,7 +13,9 @@ batch reproduces the same trajectories as the full batch.
 Auto-reset (``autoreset=True``, the default): when every done of an env is True
 the env is reset inside the same launch and the returned obs is the reset
 observation, while rewards/dones/info are the terminal ones -- the worker
-semantics of wrappers.py:139-145 (reset on ``all(done)``).
+semantics of wrappers.py:139-145 (reset on ``all(done)``). ``autoreset='every_step'``
+reproduces gym 0.23.1's worker that make_snake actually runs (wrappers.py:212):
+every env is reset after every step (rewards/dones/info of the step, the reset obs).
 """
 import ctypes
 
@@ -39,7 +41,7 @@ class SnakeVecEnv:
         self.cfg, self.meta = build_cfg(num_snakes=num_snakes, coop=coop, autoreset=autoreset,
                                         **env_kwargs)
         self.num_snakes = S = self.cfg.num_snakes
-        self.autoreset = bool(autoreset)
+        self.autoreset = autoreset if autoreset == 'every_step' else bool(autoreset)
         self.strict = bool(strict)
         self.seed_base = int(seed) & 0xffffffff
         self.env_offset = int(env_offset)

@@ -469,3 +469,28 @@ def test_vec_env_on_non_current_device():
         oa, ra, _, _ = a.step(act)
         ob, rb, _, _ = b.step(act)
         assert torch.equal(oa.cpu(), ob.cpu()) and torch.equal(ra.cpu(), rb.cpu())
+
+
+@pytest.mark.parametrize('S,kw', [(4, dict(height=20, width=20, vision_range=5)),
+                                  (2, dict(height=12, width=12, snake_length=4))])
+def test_autoreset_every_step_matches_oracle(oracle, S, kw):
+    """autoreset='every_step' (gym 0.23.1's worker behind make_snake,
+    wrappers.py:212): the step's rewards/dones/info, then a reset of every env,
+    whose obs is returned."""
+    from marlenv import SnakeVecEnv
+    N = 48
+    v = SnakeVecEnv(N, num_snakes=S, seed=21, autoreset='every_step', **kw)
+    refs, o0 = oracle_batch(oracle, N, 21, S, **kw)
+    assert (_np(v.reset()) == o0).all()
+    rs = np.random.RandomState(4)
+    for t in range(40):
+        a = rs.randint(0, 3, size=(N, S))
+        obs, rew, done, info = v.step(torch.from_numpy(a))
+        obs, rew, done = _np(obs), _np(rew), _np(done)
+        ep_done = _np(info['episode_done'])
+        for i, r in enumerate(refs):
+            _, rr, rd, rinfo = r.step(a[i])
+            assert rr.tobytes() == rew[i].tobytes(), (t, i)
+            assert (rd == done[i]).all(), (t, i)
+            assert bool(ep_done[i]) == bool(rinfo), (t, i)
+            assert (r.reset() == obs[i]).all(), (t, i)

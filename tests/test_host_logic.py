@@ -65,3 +65,13 @@ def test_render_palette_matches_reference():
     np.testing.assert_array_equal(palette(), z['palette'])
     big = upscale(z['rgb'][0])
     assert big.shape == (300, 300, 3) and (big[::15, ::15] == z['rgb'][0]).all()
+
+
+def test_autoreset_codes():
+    from marlenv.config import autoreset_code, build_cfg
+    assert autoreset_code(True) == 1 and autoreset_code(False) == 0
+    assert autoreset_code('every_step') == 2
+    with pytest.raises(ValueError):
+        autoreset_code('sometimes')
+    cfg, _ = build_cfg(autoreset='every_step')
+    assert cfg.autoreset == 2
