@@ -267,7 +267,7 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     // perm_trace): the u16 draw record in LDS up to kJarrLdsMax bytes, else one
     // global u32 link table per reset worker.
     const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
-    o->jscratch = (round_up(2 * o->n_cand, 16) <= kJarrLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
+    o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     o->spawn = N * kSpawnStride * 4;
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
         // kQShards) with room for every env of its blocks, + the step's counters
@@ -354,7 +354,8 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         k->mag_n16 = (uint32_t)(((1ull << 32) + n16 - 1) / n16);
     }
     k->link_stride = (int)round_up(k->n_cand, 4) + kWave;
-    const int jbytes = (int)round_up(2 * (int64_t)k->n_cand, 16);   // the LDS draw record
+    // the LDS draw record: u16 per index < n_cand + one dummy slot per lane
+    const int jbytes = (int)round_up(2 * ((int64_t)k->n_cand + kWave), 16);
     k->link_in_lds = jbytes <= kJarrLdsMax;
     // tuning knobs (A/B probes): workers of k_autoreset (<= kResetSlots, the
     // global link tables are sized for that) and the spawn-ahead wave priority

@@ -31,6 +31,10 @@
 
 #include "snake_internal.h"
 
+#ifndef SNAKE_RESET_WAVES_PER_EU
+#define SNAKE_RESET_WAVES_PER_EU 4   // reset workers: 128 VGPRs (3 waves/SIMD measured slower)
+#endif
+
 #ifndef SNAKE_STEP_MIN_WAVES
 #define SNAKE_STEP_MIN_WAVES 1   // waves per SIMD the step kernel is register-budgeted for
 #endif
@@ -317,74 +321,89 @@ __device__ __forceinline__ void perm_record(int ii, int w, int S, NP *link, lu16
 }
 
 // One draw round over the unread words of the register pair (tw0, tw1) at key
-// offset base (see mt_perm_draws).
+// offset base (see mt_perm_draws). Bound refinement from the possible set:
+// c = {w <= i} is a superset of the accepts, a = {w + |c before| <= i} a
+// subset; a == c settles the round (most rounds, in one pass: only a word
+// within |c before p| - A_p of its threshold stays open), else the bounds
+// alternate until they meet. The accept set's prefix counts b are the draw
+// indices' offsets, and the draw record is written through a per-lane dummy
+// slot instead of exec masking: under the step's load the worker waves are
+// issue-bound, so instructions (SALU and branches included) are the cost.
 template <typename NP>
 __device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base, WaveMT &m, int &i,
                                            uint32_t &mask, int &lo, int S, NP *link, NP *dummy,
                                            lu16 *jsmall, int lane)
 {
+    constexpr int kBig = 0x3fffffff;   // never accepted; w + b cannot overflow
     const int l0 = m.pos - base;
     const int p0 = lane - l0;   // stream offset of this lane's first word (second: + 64)
-    // words before the stream position or past the key never accept: give them
-    // an impossible value instead of masking every ballot
-    const int w0 = p0 >= 0 ? (int)(tw0 & mask) : INT_MAX;
-    const int w1 = (p0 >= -64 && base + 64 + lane < kMtN) ? (int)(tw1 & mask) : INT_MAX;
-    // a = sure accepts (upper bound: the offset), c = possible accepts (lower: 0)
-    unsigned long long a0 = __ballot(w0 <= i - p0), a1 = __ballot(w1 <= i - 64 - p0);
+    const int w0 = p0 >= 0 ? (int)(tw0 & mask) : kBig;
+    const int w1 = (p0 >= -64 && base + 64 + lane < kMtN) ? (int)(tw1 & mask) : kBig;
     unsigned long long c0 = __ballot(w0 <= i), c1 = __ballot(w1 <= i);
-    // (the empty asm keeps the test on the OR of both halves: folded into two
-    // mask compares, it costs a bool materialisation per pass)
+    int b0 = mbcnt64(c0), b1 = mbcnt64(c1, __popcll(c0));
+    unsigned long long a0 = __ballot(w0 + b0 <= i), a1 = __ballot(w1 + b1 <= i);
+    // (the empty asm keeps each test on the OR of both halves: folded into two
+    // 64-bit compares it costs two selects and an AND per test)
     unsigned long long und = (a0 ^ c0) | (a1 ^ c1);
     __asm__ volatile("" : "+s"(und));
-    while (und) {
-        const int L0 = mbcnt64(a0), U0 = mbcnt64(c0);
-        const int L1 = mbcnt64(a1, __popcll(a0)), U1 = mbcnt64(c1, __popcll(c0));
-        a0 = __ballot(w0 <= i - U0);
-        a1 = __ballot(w1 <= i - U1);
-        c0 = __ballot(w0 <= i - L0);
-        c1 = __ballot(w1 <= i - L1);
-        und = (a0 ^ c0) | (a1 ^ c1);
-        __asm__ volatile("" : "+s"(und));
+    if (__builtin_expect(und != 0ull, 0)) {
+        for (int pass = 0; pass < 128; pass++) {
+            b0 = mbcnt64(a0);
+            b1 = mbcnt64(a1, __popcll(a0));
+            c0 = __ballot(w0 + b0 <= i);
+            c1 = __ballot(w1 + b1 <= i);
+            und = (a0 ^ c0) | (a1 ^ c1);
+            __asm__ volatile("" : "+s"(und));
+            if (und == 0ull) break;
+            b0 = mbcnt64(c0);
+            b1 = mbcnt64(c1, __popcll(c0));
+            a0 = __ballot(w0 + b0 <= i);
+            a1 = __ballot(w1 + b1 <= i);
+            und = (a0 ^ c0) | (a1 ^ c1);
+            __asm__ volatile("" : "+s"(und));
+            if (und == 0ull) break;
+        }
     }
-    int A0 = __popcll(a0);
+    // a == c: b0, b1 = the accepts before each word
+    const int A0 = __popcll(a0);
     int A = A0 + __popcll(a1);
     int end = min(128, kMtN - base);
     const int k = i - lo + 1;  // accepts left in this bracket
-    if (A >= k) {
+    if (__builtin_expect(A >= k, 0)) {
         if (A0 >= k) {
-            const int b = __ffsll((long long)__ballot(inv_ballot(a0) && mbcnt64(a0) == k - 1)) - 1;
+            const int b = __ffsll((long long)__ballot(inv_ballot(a0) && b0 == k - 1)) - 1;
             a0 &= (2ull << b) - 1ull;
             a1 = 0;
-            A0 = k;
             end = b + 1;
         } else {
-            const int k1 = k - A0;
-            const int b = __ffsll((long long)__ballot(inv_ballot(a1) && mbcnt64(a1) == k1 - 1)) - 1;
+            const int b = __ffsll((long long)__ballot(inv_ballot(a1) && b1 == k - 1)) - 1;
             a1 &= (2ull << b) - 1ull;
             end = 64 + b + 1;
         }
         A = k;
     }
-    const int ii0 = i - mbcnt64(a0), ii1 = (i - A0) - mbcnt64(a1);
+    const int ii0 = i - b0, ii1 = i - b1;
     if constexpr (std::is_same<NP, lu16>::value) {
-        // LDS draw record: j_i at index i, exactly one writer per index
-        if (inv_ballot(a0)) link[ii0] = (uint16_t)w0;
-        if (inv_ballot(a1)) link[ii1] = (uint16_t)w1;
+        // LDS draw record: j_i at index i (one writer per index), the rest to
+        // the lane's dummy slot
+        *(inv_ballot(a0) ? link + ii0 : dummy) = (uint16_t)w0;
+        *(inv_ballot(a1) ? link + ii1 : dummy) = (uint16_t)w1;
     } else if (__builtin_expect(i - A + 1 < S, 0)) {   // the last rounds: some indices < S
         if (inv_ballot(a0)) perm_record(ii0, w0, S, link, jsmall);
         if (inv_ballot(a1)) perm_record(ii1, w1, S, link, jsmall);
     } else {
-        // every index of the round >= S: unconditional ds_min, misses to the dummy
+        // every index of the round >= S: unconditional min, misses to the dummy
         link_min((inv_ballot(a0) && w0 != ii0) ? link + w0 : dummy, (uint32_t)ii0);
         link_min((inv_ballot(a1) && w1 != ii1) ? link + w1 : dummy, (uint32_t)ii1);
     }
     m.pos = base + end;
     i -= A;
-    if (i < lo) {          // next power-of-two bracket (i < 1 ends the draws anyway)
+    if (__builtin_expect(i < lo, 0)) {   // next power-of-two bracket (i < 1 ends the draws anyway)
         mask = gen_mask((uint32_t)i);
         lo = (int)(mask >> 1) + 1;
     }
 }
+
 
 template <typename NP>
 __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, int lane,
@@ -1330,7 +1349,7 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
 // k_encode encodes every other env's stacked frames (bandwidth-bound, few
 // registers: full occupancy).
 template <int MS>
-__global__ void __launch_bounds__(64) k_autoreset(const KCfg c, const snake_state st, const snake_out o)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KCfg c, const snake_state st, const snake_out o)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
@@ -1808,7 +1827,7 @@ __global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsi
 
 extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, int S, unsigned long long *out_dev)
 {
-    hipLaunchKernelGGL(k_drawbench, dim3(1), dim3(64), 2 * n + 64, 0, mt_dev, pos0, n, S, out_dev);
+    hipLaunchKernelGGL(k_drawbench, dim3(1), dim3(64), 2 * n + 256, 0, mt_dev, pos0, n, S, out_dev);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
