@@ -78,7 +78,7 @@ typedef struct {
                                                          u16 draw record fits LDS (2*n_cand <= 36 KB) */
     int64_t spawn;      /* uint32 [N][656]               spawn-ahead record: MT key, MT pos and the
                                                          S spawn-pose indices of the env's next reset */
-    int64_t resetq;     /* int32  [2][64][cap] + [145*32] sharded auto-reset and spawn-ahead queues
+    int64_t resetq;     /* int32  [3][64][cap] + [209*32] sharded auto-reset and spawn-ahead queues
                                                          + the step's counters, one per 128-B line
                                                          (zero between steps) */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */

@@ -275,7 +275,7 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
         const int64_t E = kWave / (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
         const int64_t blocks = (N + E - 1) / E;
         const int64_t cap = (blocks + kQShards - 1) / kQShards * E;
-        o->resetq = (2 * kQShards * cap + kQCounters) * 4;
+        o->resetq = (kNumQ * kQShards * cap + kQCounters) * 4;
     }
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
@@ -369,6 +369,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // default 2: step 0.1275 -> 0.1200 ms at cfg3; 0 = hardware default)
     static const char *ev_eprio = getenv("SNAKE_ENCODE_PRIO");
     k->encode_prio = ev_eprio ? std::max(0, std::min(3, atoi(ev_eprio))) : 2;
+    // SNAKE_SPAWN_CAP=1: the other (2-live-snake) spawn-ahead jobs past the
+    // workers' first round wait for a later step (the urgent ones never do);
+    // off by default: measured 0.121 vs 0.109 ms at cfg3 (the hit rate falls)
+    static const char *ev_cap = getenv("SNAKE_SPAWN_CAP");
+    k->spawn_cap = ev_cap ? (atoi(ev_cap) != 0) : 0;
     k->q_envs_per_block = kWave / (k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16));
     {
         const int64_t blocks = (N + k->q_envs_per_block - 1) / k->q_envs_per_block;

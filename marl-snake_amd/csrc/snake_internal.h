@@ -27,7 +27,8 @@ constexpr int kSpawnSel = 625;      // record words [625, 625 + S): spawn-pose i
 #endif
 constexpr int kQSpread = SNAKE_QSPREAD;
 constexpr int kClaimShards = 16;    // claim counters: worker w claims on shard w % 16
-constexpr int kQClaim = 2 * kQShards;                 // counter index of claim shard 0
+constexpr int kNumQ = 3;            // queues: 0 resets, 1 urgent spawn-ahead (<= 1 live snake), 2 other spawn-ahead
+constexpr int kQClaim = kNumQ * kQShards;             // counter index of claim shard 0
 constexpr int kQDone = kQClaim + kClaimShards;        // counter index: claim shards drained
 constexpr int kQCount = kQDone + 1;                   // counters
 constexpr int kQCounters = kQCount * kQSpread;        // words
@@ -67,6 +68,7 @@ struct KCfg {
     int spawn_thr;              // queue spawn-ahead when <= this many snakes live (-1: off)
     int spawn_prio;             // wave priority of the spawn-ahead jobs (resets: 3)
     int encode_prio;            // wave priority of k_encode (beside the reset workers)
+    int spawn_cap;              // 1: other spawn-ahead jobs only in the workers' first round
     int diag;                   // count spawn-ahead hits/jobs (while timing is enabled)
     double rf, rk, rl, rw, rt, max_steps;
 };

@@ -880,7 +880,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     uint32_t *rawbuf = reinterpret_cast<uint32_t *>(lds + E * stride + 2 * kMaxFruits) + g * (G * kRespawnT);
     uint16_t *cellbuf = reinterpret_cast<uint16_t *>(lds + E * stride + 2 * kMaxFruits + E * G * kRespawnT * 4) + g * G;
     // queue counters (zero between steps: the last k_autoreset worker re-zeroes them)
-    int *qcnt = st.resetq + 2 * kQShards * c.q_cap;
+    int *qcnt = st.resetq + kNumQ * kQShards * c.q_cap;
     LSTAMP(40);
     auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
@@ -1235,9 +1235,13 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const int spst1 = (mt_slow || mtpos_new != mtpos) ? SPAWN_NONE : spst;
     const bool spawn_q = c.spawn_thr >= 0 && env_ok && !bad && !ep_end && spst1 != SPAWN_READY &&
                          __popc(am) <= c.spawn_thr;
-    const unsigned long long pm = __ballot(spawn_q && k == 0);
-    int pbase = 0;
+    // urgent (at most one live snake: the reset is likely next) and other jobs
+    const bool urgent = __popc(am) <= 1;
+    const unsigned long long pm = __ballot(spawn_q && urgent && k == 0);
+    const unsigned long long pn = __ballot(spawn_q && !urgent && k == 0);
+    int pbase = 0, nbase = 0;
     if (pm && lane == 0) pbase = atomicAdd(&qcnt[(kQShards + shard) * kQSpread], __popcll(pm));
+    if (pn && lane == 0) nbase = atomicAdd(&qcnt[(2 * kQShards + shard) * kQSpread], __popcll(pn));
 
     LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
@@ -1264,6 +1268,10 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     if (pm) {            // and the spawn-ahead jobs
         const int base = bcast(pbase, 0);
         if ((pm >> lane) & 1ull) st.resetq[(kQShards + shard) * c.q_cap + base + mbcnt64(pm)] = e;
+    }
+    if (pn) {
+        const int base = bcast(nbase, 0);
+        if ((pn >> lane) & 1ull) st.resetq[(2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn)] = e;
     }
     if (env_ok && k == 0 && !bad && spst1 != spst) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spst1;
     LSTAMP(49);
@@ -1353,26 +1361,35 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
-    // the shard counts of both queues, prefix-summed: queue index idx lives in
-    // the shard whose [excl, incl) holds it
-    int *qc = st.resetq + 2 * kQShards * c.q_cap;
-    const int cnt = qc[lane * kQSpread], pcnt = qc[(kQShards + lane) * kQSpread];
-    const int incl = wave_scan(cnt, lane), excl = incl - cnt;
-    const int pincl = wave_scan(pcnt, lane), pexcl = pincl - pcnt;
-    const int R = bcast(incl, kWave - 1), P = bcast(pincl, kWave - 1);
-    if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
-    // job idx < R: the step's resets (high priority, the critical path); idx >= R:
-    // spawn-ahead jobs. A worker's first job is its block index, the next ones
-    // are claimed once it is free (a slow reset never holds up a job another
-    // worker could take): worker w claims on shard x = w % kClaimShards, whose
-    // n-th claim is job G + x + kClaimShards * n.
+    // the shard counts of the three queues, prefix-summed: queue index j lives
+    // in the shard whose [excl, incl) holds it
+    int *qc = st.resetq + kNumQ * kQShards * c.q_cap;
+    const int cnt = qc[lane * kQSpread], ucnt = qc[(kQShards + lane) * kQSpread],
+              ncnt = qc[(2 * kQShards + lane) * kQSpread];
+    const int incl = wave_scan(cnt, lane), uincl = wave_scan(ucnt, lane), nincl = wave_scan(ncnt, lane);
+    const int R = bcast(incl, kWave - 1), U = bcast(uincl, kWave - 1);
     const int G = (int)gridDim.x, x = blockIdx.x % kClaimShards;
+    // spawn_cap: the other (2-live-snake) jobs only as far as the first round
+    // of workers reaches; their envs are queued again next step
+    int Nn = bcast(nincl, kWave - 1);
+    if (c.spawn_cap) Nn = min(Nn, max(G - R - U, 0));
+    const int P = U + Nn;
+    if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
+    // env of job j of queue q
+    auto job_env = [&](int q, int j, int qincl, int qcnt) {
+        const int sh = __ffsll((long long)__ballot(j >= qincl - qcnt && j < qincl)) - 1;
+        return st.resetq[(q * kQShards + sh) * c.q_cap + j - bcast(qincl - qcnt, sh)];
+    };
+    // job idx < R: the step's resets (high priority, the critical path); then
+    // the urgent spawn-ahead jobs, then the others. A worker's first job is its
+    // block index, the next ones are claimed once it is free (a slow reset
+    // never holds up a job another worker could take): worker w claims on
+    // shard x = w % kClaimShards, whose n-th claim is job G + x + kClaimShards * n.
     int idx = blockIdx.x, nx = 0;
     for (;;) {
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
-            const int sh = __ffsll((long long)__ballot(idx >= excl && idx < incl)) - 1;
-            const int e = st.resetq[sh * c.q_cap + idx - bcast(excl, sh)];
+            const int e = job_env(0, idx, incl, cnt);
             WaveMT mt;
             const int spst = load_reset_mt(st, e, mt, lane);
             if (c.diag && lane == 0 && spst == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
@@ -1385,8 +1402,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             else if (c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(2);
             const int j = idx - R;
-            const int sh = __ffsll((long long)__ballot(j >= pexcl && j < pincl)) - 1;
-            const int e = st.resetq[(kQShards + sh) * c.q_cap + j - bcast(pexcl, sh)];
+            const int e = j < U ? job_env(1, j, uincl, ucnt) : job_env(2, j - U, nincl, ncnt);
             if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
             if (j < 128) OBSPROF(512 + j, lane);
             if (c.link_in_lds) do_spawn<MS, true>(c, st, e, lds, blockIdx.x, lane);
