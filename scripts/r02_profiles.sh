@@ -8,7 +8,10 @@ mkdir -p gpurun_out/r02
 export TMPDIR=/tmp
 run() { local name=$1 limit=$2; shift 2; echo "== $name"; timeout -k 10 "$limit" "$@" > gpurun_out/r02/$name.log 2>&1 || { echo "$name failed rc=$?"; tail -5 gpurun_out/r02/$name.log; exit 3; }; tail -n 1 gpurun_out/r02/$name.log | cut -c1-300; }
 run bench_cfg3 300 python bench.py --cpu-seconds 10
+run bench_cfg3_2 300 python bench.py --no-cpu-baseline
 run bench_cfg3_short 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+run bench_cfg3_short2 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+run compat 200 python scripts/compat_bench.py
 run bench_cfg2 200 python bench.py --config cfg2 --no-cpu-baseline
 run bench_cfg5 200 python bench.py --config cfg5 --no-cpu-baseline
 for c in cfg3 cfg2 cfg5; do
