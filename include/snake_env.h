@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 9
+#define SNAKE_ABI_VERSION 10
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -235,6 +235,25 @@ int64_t snake_dqn_rows(const snake_dqn_cfg *cfg, int32_t *rows, int64_t n);
 int snake_dqn_forward(const snake_dqn_cfg *cfg, const snake_dqn_net *net, const uint8_t *obs,
                       int64_t batch, uint16_t *act_scratch, float *q_out, float *feat_out,
                       void *stream);
+
+/* fp32 mode of the DQN consumer (dqn32_kernels.hip): the same network in fp32
+ * arithmetic on any observation size (e.g. train_dqn.py's 20x20 full map,
+ * :29-33), cfg->channels a multiple of 8, conv_waves ignored. Weights fp32,
+ * row-major [out][in]: conv w [cout][9*cin] with k = (ky*3 + kx)*cin + ci;
+ * fc1 [256][h*w*64] with column p*64 + ch (the reference's NCHW flatten
+ * column ch*h*w + p, permuted once); fc2 [128][256]; fc3 [A][128]. The uint8
+ * input is divided by 255 when the batch holds a value > 1 (train_dqn.py:122). */
+typedef struct {
+    const float *conv1_w, *conv2_w, *conv3_w, *fc1_w, *fc2_w, *fc3_w;
+    const float *conv1_b, *conv2_b, *conv3_b, *fc1_b, *fc2_b, *fc3_b;
+} snake_dqn32_net;
+
+/* Device scratch bytes snake_dqn32_forward needs for `batch` observations (< 0 on error). */
+int64_t snake_dqn32_scratch(const snake_dqn_cfg *cfg, int64_t batch);
+
+/* q_out: float [B][A]; feat_out (may be NULL): float [B][128]. Seven launches on `stream`. */
+int snake_dqn32_forward(const snake_dqn_cfg *cfg, const snake_dqn32_net *net, const uint8_t *obs,
+                        int64_t batch, void *scratch, float *q_out, float *feat_out, void *stream);
 
 /* Last error message of this thread ("" if none). */
 const char *snake_last_error(void);

@@ -10,12 +10,12 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 9
+SNAKE_ABI_VERSION = 10
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
            'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version',
-           'snake_dqn_plan', 'snake_dqn_rows', 'snake_dqn_forward')
+           'snake_dqn_plan', 'snake_dqn_rows', 'snake_dqn_forward', 'snake_dqn32_scratch', 'snake_dqn32_forward')
 
 
 class SnakeCfg(ctypes.Structure):
@@ -64,6 +64,12 @@ class DqnNet(ctypes.Structure):
         'fc3_w', 'fc3_b')]
 
 
+class Dqn32Net(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        'conv1_w', 'conv2_w', 'conv3_w', 'fc1_w', 'fc2_w', 'fc3_w', 'conv1_b', 'conv2_b', 'conv3_b', 'fc1_b',
+        'fc2_b', 'fc3_b')]
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -103,6 +109,9 @@ def lib(path=None):
     L.snake_dqn_rows.argtypes = [ctypes.POINTER(DqnCfg), P, I64]
     L.snake_dqn_rows.restype = I64
     L.snake_dqn_forward.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(DqnNet), P, I64, P, P, P, P]
+    L.snake_dqn32_scratch.argtypes = [ctypes.POINTER(DqnCfg), I64]
+    L.snake_dqn32_scratch.restype = I64
+    L.snake_dqn32_forward.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(Dqn32Net), P, I64, P, P, P, P]
     L.snake_timing_enable.argtypes = [ctypes.c_int]
     L.snake_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_int64)]

@@ -17,7 +17,7 @@ torch ops, the forward pass is the HIP kernels only.
 """
 import ctypes
 
-from ._native import DqnCfg, DqnLayout, DqnNet, check, lib
+from ._native import Dqn32Net, DqnCfg, DqnLayout, DqnNet, check, lib
 
 
 def _torch():
@@ -29,15 +29,27 @@ class DQNForward:
     """DQN(input_shape=(N, h, w, c), num_actions) forward on uint8 NHWC observations.
 
     state: a state dict (or nn.Module) of the reference DQN (conv1..conv3, fc1..fc3).
-    conv_waves: waves per observation in the conv kernel (0 = the library default)."""
+    conv_waves: waves per observation in the conv kernel (0 = the library default).
+    precision: 'bf16' (the fused MFMA kernels: bf16 products, fp32 accumulation;
+    square odd maps up to 11x11, 8-32 channels) or 'fp32' (dqn32_kernels.hip:
+    fp32 arithmetic on any map, e.g. train_dqn.py's 20x20 full-map Config)."""
 
-    def __init__(self, state, height, width, channels, num_actions=3, device=None, lib_path=None, conv_waves=0):
+    def __init__(self, state, height, width, channels, num_actions=3, device=None, lib_path=None, conv_waves=0,
+                 precision='bf16'):
         torch = _torch()
         if hasattr(state, 'state_dict'):
             state = state.state_dict()
         self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
         self._L = L = lib(lib_path)
         self.cfg = DqnCfg(int(height), int(width), int(channels), int(num_actions), int(conv_waves))
+        if precision not in ('bf16', 'fp32'):
+            raise ValueError("precision must be 'bf16' or 'fp32'")
+        self.precision = precision
+        self.num_actions = int(num_actions)
+        self._scratch = None
+        if precision == 'fp32':
+            self._init_fp32(state)
+            return
         lay = DqnLayout()
         check(L.snake_dqn_plan(ctypes.byref(self.cfg), ctypes.byref(lay)), L)
         self.layout = lay
@@ -99,6 +111,40 @@ class DQNForward:
         self.num_actions = A
         self._scratch = None
 
+    def _init_fp32(self, state):
+        """fp32 weights, row-major [out][in] (include/snake_env.h snake_dqn32_net);
+        fc1's columns permuted from the NCHW flatten to NHWC."""
+        torch = _torch()
+        H, W, C, A = self.cfg.height, self.cfg.width, self.cfg.channels, self.cfg.num_actions
+        P = H * W
+        n = self._L.snake_dqn32_scratch(ctypes.byref(self.cfg), 0)
+        check(int(n) if n < 0 else 0, self._L)
+        f32 = dict(dtype=torch.float32, device=self.device)
+
+        def g(name):
+            return state[name].detach().to(**f32)
+
+        def conv(w, cin):
+            if tuple(w.shape[1:]) != (cin, 3, 3):
+                raise ValueError('conv weight shape %s does not match %d input channels' % (tuple(w.shape), cin))
+            return w.permute(0, 2, 3, 1).reshape(w.shape[0], 9 * cin).contiguous()
+        fc1 = g('fc1.weight')
+        if tuple(fc1.shape) != (256, 64 * P):
+            raise ValueError('fc1.weight shape %s != (256, %d)' % (tuple(fc1.shape), 64 * P))
+        fc3 = g('fc3.weight')
+        if tuple(fc3.shape) != (A, 128):
+            raise ValueError('fc3.weight shape %s != (%d, 128)' % (tuple(fc3.shape), A))
+        self.tensors = dict(
+            conv1_w=conv(g('conv1.weight'), C), conv2_w=conv(g('conv2.weight'), 32),
+            conv3_w=conv(g('conv3.weight'), 64),
+            fc1_w=fc1.reshape(256, 64, P).permute(0, 2, 1).reshape(256, P * 64).contiguous(),
+            fc2_w=g('fc2.weight').contiguous(), fc3_w=fc3.contiguous(),
+            conv1_b=g('conv1.bias'), conv2_b=g('conv2.bias'), conv3_b=g('conv3.bias'),
+            fc1_b=g('fc1.bias'), fc2_b=g('fc2.bias'), fc3_b=g('fc3.bias'))
+        self.net = Dqn32Net(*(self.tensors[k].data_ptr() for k in (
+            'conv1_w', 'conv2_w', 'conv3_w', 'fc1_w', 'fc2_w', 'fc3_w', 'conv1_b', 'conv2_b', 'conv3_b',
+            'fc1_b', 'fc2_b', 'fc3_b')))
+
     def _run(self, obs, features):
         torch = _torch()
         H, W, C = self.cfg.height, self.cfg.width, self.cfg.channels
@@ -109,6 +155,8 @@ class DQNForward:
             raise TypeError('DQNForward takes the env observations as uint8 (got %s)' % obs.dtype)
         obs = obs.to(self.device).contiguous()
         B = obs.shape[0]
+        if self.precision == 'fp32':
+            return self._run32(obs, B, features)
         need = B * self.layout.act_per_obs
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.int16, device=self.device)
@@ -120,6 +168,23 @@ class DQNForward:
                                         ctypes.c_void_p(self._scratch.data_ptr()),
                                         ctypes.c_void_p(q.data_ptr()),
                                         ctypes.c_void_p(feat.data_ptr()) if features else None, stream), self._L)
+        self._keep = obs
+        return q, feat
+
+    def _run32(self, obs, B, features):
+        torch = _torch()
+        need = int(self._L.snake_dqn32_scratch(ctypes.byref(self.cfg), B))
+        check(need if need < 0 else 0, self._L)
+        if self._scratch is None or self._scratch.numel() < need:
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+        q = torch.empty((B, self.num_actions), dtype=torch.float32, device=self.device)
+        feat = torch.empty((B, 128), dtype=torch.float32, device=self.device) if features else None
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        check(self._L.snake_dqn32_forward(ctypes.byref(self.cfg), ctypes.byref(self.net),
+                                          ctypes.c_void_p(obs.data_ptr()), B,
+                                          ctypes.c_void_p(self._scratch.data_ptr()),
+                                          ctypes.c_void_p(q.data_ptr()),
+                                          ctypes.c_void_p(feat.data_ptr()) if features else None, stream), self._L)
         self._keep = obs
         return q, feat
 

@@ -12,7 +12,7 @@ for spec in "$@"; do
     if [[ $spec == *@* ]]; then
         tag=${spec%@*}; rev=${spec#*@}
         src=$OUT/src_$tag; mkdir -p "$src/csrc" "$src/include"
-        for f in snake_kernels.hip snake_capi.cpp snake_internal.h dqn_kernels.hip; do
+        for f in snake_kernels.hip snake_capi.cpp snake_internal.h dqn_kernels.hip dqn32_kernels.hip; do
             git -C "$ROOT" show "$rev:marl-snake_amd/csrc/$f" > "$src/csrc/$f"
         done
         git -C "$ROOT" show "$rev:include/snake_env.h" | sed "s/define SNAKE_ABI_VERSION .*/define SNAKE_ABI_VERSION ${ABI:-8}/" > "$src/include/snake_env.h"
@@ -22,7 +22,7 @@ for spec in "$@"; do
         tag=${spec%%:*}; extra=${spec#*:}; dir=$ROOT/marl-snake_amd/csrc
         [[ $extra == "$spec" ]] && extra=""
     fi
-    dqn=""; [[ -f $dir/dqn_kernels.hip ]] && dqn=$dir/dqn_kernels.hip
+    dqn=""; [[ -f $dir/dqn_kernels.hip ]] && dqn=$dir/dqn_kernels.hip; [[ -f $dir/dqn32_kernels.hip ]] && dqn="$dqn $dir/dqn32_kernels.hip"
     /opt/rocm/bin/hipcc $FLAGS $extra -shared -o "$OUT/libsnake_$tag.so" "$dir/snake_kernels.hip" "$dir/snake_capi.cpp" $dqn &
 done
 wait

@@ -25,6 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, 'tests'))
 import torch  # noqa: E402
 
 PEAK_BF16 = 2.5e15
+PEAK_FP32 = 157.3e12   # MI355X fp32 (vector and matrix)
 
 
 def flops_per_obs(h, w, c, a):
@@ -54,6 +55,7 @@ def main():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--no-torch', action='store_true')
+    ap.add_argument('--precision', choices=('bf16', 'fp32'), default='bf16')
     args = ap.parse_args()
 
     from marlenv import SnakeVecEnv
@@ -62,7 +64,7 @@ def main():
 
     torch.manual_seed(0)
     env = SnakeVecEnv(args.envs, num_snakes=args.snakes, seed=0, height=20, width=20,
-                      vision_range=args.vr, frame_stack=args.fs)
+                      vision_range=args.vr or None, frame_stack=args.fs)   # --vr 0: full 20x20 map
     env.reset()
     g = torch.Generator(device='cuda').manual_seed(0)
     for _ in range(8):
@@ -72,16 +74,18 @@ def main():
     B, h, w, c = obs.shape
     del env
     ref = RefDQN(h, w, c, 3).cuda().eval()
-    net = DQNForward(ref, h, w, c, 3)
+    net = DQNForward(ref, h, w, c, 3, precision=args.precision)
     fpo = flops_per_obs(h, w, c, 3)
+    peak = PEAK_BF16 if args.precision == 'bf16' else PEAK_FP32
 
     ms = timed(lambda: net(obs), args.steps, args.warmup)
     tf = fpo * B / (ms * 1e-3)
     out = {'metric': 'dqn_forward_obs_per_sec', 'value': B / (ms * 1e-3), 'unit': 'obs/s',
-           'ms_per_forward': ms, 'batch': B, 'obs_shape': [h, w, c], 'dtype': 'bf16 (fp32 accumulate)',
+           'ms_per_forward': ms, 'batch': B, 'obs_shape': [h, w, c],
+           'dtype': 'bf16 (fp32 accumulate)' if args.precision == 'bf16' else 'fp32',
            'flop_per_obs': fpo,
-           'roofline': {'bound': 'mfma', 'achieved': tf / 1e12, 'peak': PEAK_BF16 / 1e12, 'unit': 'TFLOP/s',
-                        'frac': tf / PEAK_BF16}}
+           'roofline': {'bound': 'mfma' if args.precision == 'bf16' else 'fp32 (vector = matrix peak)',
+                        'achieved': tf / 1e12, 'peak': peak / 1e12, 'unit': 'TFLOP/s', 'frac': tf / peak}}
     if not args.no_torch:
         with torch.no_grad():
             ms32 = timed(lambda: ref(obs), max(3, args.steps // 4), 2)

@@ -1,7 +1,11 @@
 """The fused DQN consumer (marl-snake_amd/csrc/dqn_kernels.hip) against a plain
 PyTorch fp32 restatement of the reference network (train_dqn.py:104-151).
 
-Tolerance: the matrix products take bf16 inputs (weights and activations are
+fp32 mode (precision='fp32', dqn32_kernels.hip): fp32 arithmetic on any map
+(train_dqn.py's 20x20 full-map Config included); held to |err| <= 1e-5 * max|ref|
+against a float64 CPU restatement (no reduced-precision conv/matmul paths).
+
+Tolerance (bf16 mode): the matrix products take bf16 inputs (weights and activations are
 rounded to bf16 between layers, 8 significant bits) with fp32 accumulation, so
 outputs agree with the fp32 reference to |err| <= 2e-2 * max|ref| + 1e-3 (a
 bf16-emulating reference agrees to <= 2e-3 * max|ref|, which pins the layouts)."""
@@ -26,7 +30,7 @@ class RefDQN(nn.Module):
 
     def forward_features(self, x, bf16=False):
         r = (lambda t: t.to(torch.bfloat16).float()) if bf16 else (lambda t: t)
-        x = x.permute(0, 3, 1, 2).float()
+        x = x.permute(0, 3, 1, 2).to(self.conv1.weight.dtype)   # .float() (float64 for the fp32-mode check)
         x = x / 255.0 if x.max() > 1.0 else x
         def lin(layer, t):
             return F.linear(r(t), r(layer.weight), layer.bias)
@@ -143,3 +147,62 @@ def test_dqn_full_batch_sampled():
     scale = float(q32.abs().max())
     assert torch.isfinite(q).all()
     assert float((q[rows] - q32).abs().max()) <= 2e-2 * scale + 1e-3
+
+
+def _obs_full(B, fs=1, S=4, seed=0, H=20, W=20):
+    """Full-map observations (vision_range None) of a short GPU rollout."""
+    from marlenv import SnakeVecEnv
+    n = max(1, -(-B // S))
+    v = SnakeVecEnv(n, num_snakes=S, seed=seed, height=H, width=W, frame_stack=fs)
+    v.reset()
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    for _ in range(12):
+        o, _, _, _ = v.step(torch.randint(0, 3, (n, S), generator=g, device='cuda', dtype=torch.int8))
+    return o.reshape(-1, *o.shape[2:])[:B].contiguous()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,shape,full', [(64, (20, 20, 8), True), (37, (20, 20, 16), True), (1, (20, 20, 8), True),
+                                          (300, (11, 11, 8), False), (50, (11, 11, 32), False),
+                                          (20, (12, 10, 8), True)])
+def test_dqn_fp32_matches_reference(B, shape, full):
+    """precision='fp32' against the reference network in float64 on the CPU,
+    |err| <= 1e-5 * max|q| (train_dqn.py's own Config: 20x20x8 full map)."""
+    from marlenv.dqn import DQNForward
+    h, w, c = shape
+    torch.manual_seed(2)
+    ref = RefDQN(h, w, c, 3)
+    if full:
+        obs = _obs_full(B, fs=c // 8, H=h, W=w)
+    else:
+        obs = _obs_batch(B, (h - 1) // 2, c // 8)
+    assert obs.shape == (B, h, w, c)
+    net = DQNForward(ref.cuda(), h, w, c, 3, precision='fp32')
+    q = net(obs)
+    feat = net.forward_features(obs)
+    torch.cuda.synchronize()
+    ref64 = ref.double().cpu()
+    with torch.no_grad():
+        x = obs.cpu()
+        q64 = ref64(x.double())
+        f64 = ref64.forward_features(x.double())
+    scale, fscale = float(q64.abs().max()), float(f64.abs().max())
+    assert float((q.double().cpu() - q64).abs().max()) <= 1e-5 * scale
+    assert float((feat.double().cpu() - f64).abs().max()) <= 1e-5 * fscale
+
+
+@pytest.mark.gpu
+def test_dqn_fp32_scales_large_inputs():
+    """uint8 inputs above 1 are divided by 255 (train_dqn.py:122), as one batch."""
+    from marlenv.dqn import DQNForward
+    torch.manual_seed(4)
+    ref = RefDQN(6, 6, 8, 2)
+    g = torch.Generator(device='cuda').manual_seed(9)
+    obs = torch.randint(0, 256, (9, 6, 6, 8), generator=g, device='cuda', dtype=torch.uint8)
+    net = DQNForward(ref.cuda(), 6, 6, 8, 2, precision='fp32')
+    q = net(obs)
+    torch.cuda.synchronize()
+    ref64 = ref.double().cpu()
+    with torch.no_grad():
+        q64 = ref64(obs.cpu().double())
+    assert float((q.double().cpu() - q64).abs().max()) <= 1e-5 * float(q64.abs().max())
