@@ -138,7 +138,10 @@ int snake_seed(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
                uint32_t base_seed, int64_t env_offset, void *stream);
 
 /* SnakeEnv.reset() (snake_env.py:131-159) for every env whose env_mask byte is
- * nonzero (env_mask == NULL: all envs); writes out->obs for those envs. */
+ * nonzero (env_mask == NULL: all envs); writes out->obs for those envs. With
+ * spawn-ahead on (autoreset on all-done, cfg->spawn_ahead != -1) each reset env
+ * also gets the spawn poses of its NEXT reset drawn into its spawn record (up to
+ * 4 permutation attempts: status ready, else partial), see snake_step. */
 int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
                 const uint8_t *env_mask, const snake_out *out, void *stream);
 

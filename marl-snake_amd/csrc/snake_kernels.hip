@@ -1330,14 +1330,10 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
 // attempt of its next reset, from its MT state or its partial record, into the
 // record. k_logic queues only envs with no ready record whose reset is not this
 // step, so nothing else touches the env's MT state or record meanwhile.
-template <int MS, bool JL>
-__device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot, int lane)
+template <int MS>
+__device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, const WaveMT &mt, bool ok,
+                                   const int (&q)[MS], int lane)
 {
-    WaveMT mt;
-    const int spst = load_reset_mt(st, e, mt, lane);
-    if (spst == SPAWN_READY) return;
-    int q[MS], cell;
-    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, 0, q, cell, lane);
     uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
     mt_store(mt, rec, lane);
     int mine = 0;
@@ -1348,6 +1344,36 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
         rec[kSpawnPos] = (uint32_t)mt.pos;
         st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = ok ? SPAWN_READY : SPAWN_PARTIAL;
     }
+}
+
+template <int MS, bool JL>
+__device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot, int lane)
+{
+    WaveMT mt;
+    const int spst = load_reset_mt(st, e, mt, lane);
+    if (spst == SPAWN_READY) return;
+    int q[MS], cell;
+    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, 0, q, cell, lane);
+    store_spawn_record<MS>(c, st, e, mt, ok, q, lane);
+}
+
+// Spawn-ahead right after an explicit reset (k_reset): the next episode's spawn
+// poses drawn from the MT state the reset leaves (still in registers), up to
+// kResetAheadTries permutation attempts (READY, else a PARTIAL record the step's
+// workers continue). Nothing else has drawn from that state, so the record is
+// exactly what the next reset would draw (spawn-ahead semantics, snake_step).
+constexpr int kResetAheadTries = 4;
+
+template <int MS, bool JL>
+__device__ void spawn_after_reset(const KCfg &c, const snake_state &st, int e, WaveMT &mt, uint8_t *lds,
+                                  int slot, int lane)
+{
+    wave_sync();   // the reset's encode has read the LDS frames the draw record may overlay
+    int q[MS], cell;
+    bool ok = false;
+    for (int a = 0; a < kResetAheadTries && !ok; a++)
+        ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, a, q, cell, lane);
+    store_spawn_record<MS>(c, st, e, mt, ok, q, lane);
 }
 
 // ---------------------------------------------------- step: the observation
@@ -1374,6 +1400,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     int Nn = bcast(nincl, kWave - 1);
     if (c.spawn_cap) Nn = min(Nn, max(G - R - U, 0));
     const int P = U + Nn;
+    const int T = R + P;
     if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
     // env of job j of queue q
     auto job_env = [&](int q, int j, int qincl, int qcnt) {
@@ -1413,7 +1440,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         if (lane == 0) v = atomicAdd(&qc[(kQClaim + x) * kQSpread], 1);
         nx = bcast(v, 0);
         idx = G + x + kClaimShards * nx;
-        if (idx >= R + P) break;
+        if (idx >= T) break;
     }
     // Every worker ends with exactly one failing claim, so the shard's claims
     // number its jobs + its workers, and the worker whose failing claim is the
@@ -1421,7 +1448,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     // step's counters for the next step: every worker has read its counts and
     // made its last claim by then (no host-side step parity, one extra atomic
     // per shard).
-    const int jobs_x = R + P > G + x ? (R + P - G - x + kClaimShards - 1) / kClaimShards : 0;
+    const int jobs_x = T > G + x ? (T - G - x + kClaimShards - 1) / kClaimShards : 0;
     const int workers_x = (G - x + kClaimShards - 1) / kClaimShards;
     if (nx == jobs_x + workers_x - 1) {
         int d = 0;
@@ -1472,6 +1499,11 @@ __global__ void __launch_bounds__(64) k_reset(const KCfg c, const snake_state st
         const int spst = load_reset_mt(st, e, mt, lane);
         if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
         else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
+        // with spawn-ahead on, the next reset's poses are drawn now, off the step
+        if (c.spawn_thr >= 0) {
+            if (c.link_in_lds) spawn_after_reset<MS, true>(c, st, e, mt, lds, blockIdx.x, lane);
+            else spawn_after_reset<MS, false>(c, st, e, mt, lds, blockIdx.x, lane);
+        }
     }
 }
 
