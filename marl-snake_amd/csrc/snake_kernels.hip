@@ -1033,6 +1033,60 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         rew = r;
     }
 
+    // ---- the step's second round of memory accesses, all issued here: their
+    // addresses are known once the rules are, and in program order each group
+    // cost the wave a memory round trip of its own. The tail-queue refill of a
+    // snake that empties its queue (at the head slot after this step's push),
+    // the first 16 body directions of a dying snake, the fruit-respawn raw words
+    // of an env that needs a fruit, and the spawn-ahead queue claims.
+    // per env (all G lanes of the group, snake or not): a fruit respawn
+    const bool need = env_ok && !bad && fruit_taken > 0;
+    // spawn-ahead (include/snake_env.h): a draw from the MT state voids the env's
+    // record; an env near its episode end without a ready record is queued for
+    // one attempt of its next reset (this step's k_autoreset workers). Claimed
+    // as if every respawn drew (a queued env whose record stays ready is skipped
+    // by its job); the status word written below is the exact one.
+    const bool spawn_q = c.spawn_thr >= 0 && env_ok && !bad && !ep_end && (need ? true : spst != SPAWN_READY) &&
+                         __popc(am) <= c.spawn_thr;
+    // urgent (at most one live snake: the reset is likely next) and other jobs
+    const bool urgent = __popc(am) <= 1;
+    const unsigned long long pm = __ballot(spawn_q && urgent && k == 0);
+    const unsigned long long pn = __ballot(spawn_q && !urgent && k == 0);
+    int pbase = 0, nbase = 0;
+    if (pm && lane == 0) pbase = atomicAdd(&qcnt[(kQShards + shard) * kQSpread], __popcll(pm));
+    if (pn && lane == 0) nbase = atomicAdd(&qcnt[(2 * kQShards + shard) * kQSpread], __popcll(pn));
+
+    uint8_t *ring = st.body + ((int64_t)e * S + k) * cap;
+    const bool refill = alive && !eat && (tq >> 28) == 1u;
+    const int rt1 = (((rh - 1) & (cap - 1)) + rl - 1) & (cap - 1), rbase = rt1 & ~7;
+    uint64_t rchunk = 0;
+    if (refill) rchunk = *reinterpret_cast<const uint64_t *>(ring + rbase);
+    const bool dying = isn && death;
+    int dd[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) dd[t] = (dying && t < rl - 1) ? ring[(rh + t) & (cap - 1)] : 0;
+    // the next G * kRespawnT raw words of the stream; past the key's end they
+    // are words of the next key, computed from the old one (new[j] for j < 227
+    // needs old[j], old[j+1] and old[j+397] only): the twist is left pending in
+    // the stored position (> 624), every MT consumer applies it
+    const bool room = mtpos + G * kRespawnT <= kMtN + 226;
+    uint32_t raws[kRespawnT];
+    {
+        const uint32_t *key = st.mt + (int64_t)e * kMtN;
+#pragma unroll
+        for (int t = 0; t < kRespawnT; t++) {
+            const int pw = mtpos + t * G + k;
+            raws[t] = 0u;
+            if (need && room) {
+                if (pw < kMtN) {
+                    raws[t] = key[pw];
+                } else {
+                    const int j = pw - kMtN;
+                    raws[t] = mt_mix(key[j], key[j + 1], key[j + 397]);
+                }
+            }
+        }
+    }
     // _update_grid in two phases. Phase 1: every tail that leaves its cell is
     // cleared if it still holds this snake's TAIL, and every dying snake's tail
     // if it is still this snake's; phase 2: BODY at the old head, HEAD at the
@@ -1048,7 +1102,6 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         if (div10(work[pt]) == k) work[pt] = C_EMPTY;
     }
     wave_sync();
-    uint8_t *ring = st.body + ((int64_t)e * S + k) * cap;
     int nhr = hr, nhc = hc, ntr = tr, ntc = tc;
     if (alive) {
         work[hr * W + hc] = (uint8_t)(C_BODY + 10 * k);
@@ -1057,6 +1110,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         rh = (rh - 1) & (cap - 1);                                   // directions.appendleft
         const int ho = rh & 3;
         hbuf = (hbuf & ~(3 << (2 * ho))) | (dir << (2 * ho));
+        const int hfull = hbuf;                                      // the head word's directions
         if (ho == 0) {                                               // the head word is complete
             *reinterpret_cast<uint32_t *>(ring + rh) = (uint32_t)(hbuf & 3) | ((uint32_t)(hbuf >> 2 & 3) << 8) |
                                                        ((uint32_t)(hbuf >> 4 & 3) << 16) |
@@ -1072,15 +1126,16 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
                 // refill from the chunk holding the new directions[-1] (position t):
                 // t, t-1, .. down to the chunk start, but not below the head (the
                 // positions past it are free ring slots); pending head-word bytes
-                // come from hbuf
-                const int t = (rh + rl - 1) & (cap - 1), base = t & ~7;
-                const uint64_t q = *reinterpret_cast<const uint64_t *>(ring + base);
+                // come from the head word's directions
+                const int t = rt1, base = rbase;   // (t = rh + rl - 1 with the new rh)
+                const uint64_t q = rchunk;
                 const int n = min(t - base + 1, ((t - rh) & (cap - 1)) + 1);
                 uint32_t nq = 0;
                 for (int j = 0; j < n; j++) {
                     const int p = t - j;
                     int d = (int)(q >> (8 * (p - base))) & 3;
-                    if (ho != 0 && (p >> 2) == (rh >> 2) && p >= rh) d = (hbuf >> (2 * (p & 3))) & 3;
+                    // (the chunk was read before this step's head-word store)
+                    if ((p >> 2) == (rh >> 2) && p >= rh) d = (hfull >> (2 * (p & 3))) & 3;
                     nq |= (uint32_t)d << (2 * j);
                 }
                 tq = nq | ((uint32_t)n << 28);
@@ -1097,15 +1152,15 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // (core/snake.py:86-94). Every dying snake walks its own body on its lane, 16
     // ring bytes fetched per memory round trip.
     LSTAMP(43);
-    if (isn && death) {
-        const uint8_t *rk = st.body + ((int64_t)e * S + k) * cap;
+    if (dying) {
+        const uint8_t *rk = ring;
         int br = hr, bc = hc;
         work[br * W + bc] = C_EMPTY;
         const int n = rl - 1;
         for (int m0 = 0; m0 < n; m0 += 16) {
             int d[16];
 #pragma unroll
-            for (int t = 0; t < 16; t++) d[t] = (m0 + t < n) ? rk[(rh + m0 + t) & (cap - 1)] : 0;
+            for (int t = 0; t < 16; t++) d[t] = (m0 == 0) ? dd[t] : ((m0 + t < n) ? rk[(rh + m0 + t) & (cap - 1)] : 0);
             if (m0 == 0 && (rh & 3) != 0) {                          // the pending head-word bytes
 #pragma unroll
                 for (int t = 0; t < 3; t++)
@@ -1131,8 +1186,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // slice of the grid and the v-th one found by the lane whose slice holds it.
     int mtpos_new = mtpos;
     bool mt_slow = false;
-    // per env (all G lanes of the group, snake or not): the empties are counted by all
-    const bool need = env_ok && !bad && fruit_taken > 0;
+    // (per env, all G lanes of the group, snake or not: the empties are counted by all)
     bool fast_done = false;
     if (__ballot(need)) {
         const int HW = c.HW, nw = (HW + 3) >> 2, wpl = (nw + G - 1) / G;
@@ -1153,25 +1207,11 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         const uint32_t rng = (uint32_t)(Etot - 1), rmask = gen_mask(rng);
         // rng == 0 draws nothing (randint(0, 1) consumes no raw word)
         const bool draws = need && Etot > 0 && rng != 0;
-        // the next G * kRespawnT raw words of the stream; past the key's end they
-        // are words of the next key, computed from the old one (new[j] for
-        // j < 227 needs old[j], old[j+1] and old[j+397] only): the twist is left
-        // pending in the stored position (> 624), every MT consumer applies it
-        const bool room = mtpos + G * kRespawnT <= kMtN + 226;
-        const uint32_t *key = st.mt + (int64_t)e * kMtN;
+        // the raw words were loaded with the second round (above)
         uint32_t accm = 0;
 #pragma unroll
         for (int t = 0; t < kRespawnT; t++) {
-            const int pw = mtpos + t * G + k;
-            uint32_t raw = 0u;
-            if (draws && room) {
-                if (pw < kMtN) {
-                    raw = key[pw];
-                } else {
-                    const int j = pw - kMtN;
-                    raw = mt_mix(key[j], key[j + 1], key[j + 397]);
-                }
-            }
+            const uint32_t raw = (draws && room) ? raws[t] : 0u;
             const uint32_t tv = temper(raw) & rmask;
             rawbuf[t * G + k] = tv;
             accm |= gbits(__ballot(draws && room && tv <= rng)) << (t * G);
@@ -1229,19 +1269,8 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         mt_store(mt, st.mt + ee * kMtN, lane);
         if (g == gg) { mtpos_new = mt.pos; mt_slow = true; }
     }
-    // spawn-ahead (include/snake_env.h): a draw from the MT state voids the env's
-    // record; an env near its episode end without a ready record is queued for
-    // one attempt of its next reset (this step's k_autoreset workers)
+    // a draw from the MT state voids the env's spawn-ahead record
     const int spst1 = (mt_slow || mtpos_new != mtpos) ? SPAWN_NONE : spst;
-    const bool spawn_q = c.spawn_thr >= 0 && env_ok && !bad && !ep_end && spst1 != SPAWN_READY &&
-                         __popc(am) <= c.spawn_thr;
-    // urgent (at most one live snake: the reset is likely next) and other jobs
-    const bool urgent = __popc(am) <= 1;
-    const unsigned long long pm = __ballot(spawn_q && urgent && k == 0);
-    const unsigned long long pn = __ballot(spawn_q && !urgent && k == 0);
-    int pbase = 0, nbase = 0;
-    if (pm && lane == 0) pbase = atomicAdd(&qcnt[(kQShards + shard) * kQSpread], __popcll(pm));
-    if (pn && lane == 0) nbase = atomicAdd(&qcnt[(2 * kQShards + shard) * kQSpread], __popcll(pn));
 
     LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
