@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 10
+#define SNAKE_ABI_VERSION 11
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -71,7 +71,7 @@ typedef struct {
                                                          spawn-ahead status (0 none, 1 partial, 2 ready),
                                                          spawn failure (1: the last reset gave up, below) */
     int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */
-    int64_t stats;      /* double [N][4][S]              episode scores/steps/fruits/kills */
+    int64_t stats;      /* snake_epi_stat [N][S]         running episode score/steps/fruits/kills */
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
     int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
     int64_t jscratch;   /* uint32 [min(N,2560)][round4(n_cand)+64] reset link tables, 0 when the
@@ -95,13 +95,24 @@ typedef struct {
     int32_t grid_stride, ring_cap;
 } snake_layout;
 
+/* Running episode statistics of one snake (_reset_epi_stats, snake_env.py:
+ * 385-389, 438-442): the score in float64 as the reference sums it; steps,
+ * fruits and kills are the reference's integer-valued float64 sums held as
+ * integers (fruits < 65536: a snake's length is bounded by the board; kills
+ * <= num_snakes: every kill credit is a death in the episode). */
+typedef struct {
+    double   score;
+    uint32_t steps;
+    uint16_t fruits, kills;
+} snake_epi_stat;
+
 typedef struct {        /* device state buffers (layouts in snake_layout) */
     uint8_t  *grid;
     int32_t  *snake;
     uint8_t  *body;
     int32_t  *env;
     uint16_t *ctr;
-    double   *stats;
+    snake_epi_stat *stats;
     uint32_t *mt;
     const int16_t *cand;
     uint32_t *jscratch; /* may be NULL when layout.jscratch == 0 */

@@ -260,7 +260,7 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->body = N * S * o->ring_cap;
     o->env = N * kEnvRec * 4;
     o->ctr = N * fs * S * 2;
-    o->stats = N * 4 * S * 8;
+    o->stats = N * S * (int64_t)sizeof(snake_epi_stat);
     o->mt = N * kMtN * 4;
     o->cand = o->n_cand * c->snake_length * 2;
     // What the reset workers record of a permutation (snake_kernels.hip

@@ -821,7 +821,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         st.env[(int64_t)e * kEnvRec + ENV_FAIL] = failed ? 1 : 0;
         if (failed && o.err) o.err[e] = 2;
     }
-    if (lane < 4 * S) st.stats[(int64_t)e * 4 * S + lane] = 0.0;   // _reset_epi_stats
+    if (lane < 2 * S) reinterpret_cast<uint64_t *>(st.stats)[(int64_t)e * 2 * S + lane] = 0ull;   // _reset_epi_stats
     mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
     wave_sync();
     STAMP(e, lane, 22);
@@ -895,12 +895,13 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     }
     int4 rec = make_int4(0, 0, 0, 0);
     int act = 0;
-    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    double *sp = st.stats + (int64_t)e * 4 * S;
+    // the snake's running episode statistics, one 16-byte record (snake_epi_stat)
+    uint4 sv = make_uint4(0, 0, 0, 0);
+    uint4 *sp = reinterpret_cast<uint4 *>(st.stats) + (int64_t)e * S + k;
     if (isn) {
         rec = reinterpret_cast<const int4 *>(st.snake)[(int64_t)e * S + k];
         act = actions[(int64_t)e * S + k];
-        s0 = sp[k]; s1 = sp[S + k]; s2 = sp[2 * S + k]; s3 = sp[3 * S + k];
+        sv = *sp;
     }
     const int alive0 = er.x, eplen = er.y, cur = er.z, mtpos = er.w;
     // stage the E current frames (env g's at lds + g * stride): eight 16-B loads
@@ -933,7 +934,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     else stage(std::false_type{});
     // keep the statistics loads up here with the others (the compiler would sink
     // them to their first use, deep in the step, and pay a full memory latency there)
-    __asm__ volatile("" ::"v"(s0), "v"(s1), "v"(s2), "v"(s3));
+    __asm__ volatile("" ::"v"(sv.x), "v"(sv.y), "v"(sv.z), "v"(sv.w));
+    double s0 = __hiloint2double((int)sv.y, (int)sv.x);
+    uint32_t s1 = sv.z, s2 = sv.w & 0xffffu, s3 = sv.w >> 16;
     const int ncur = (fs == 1) ? 0 : (cur + 1 == fs ? 0 : cur + 1);
     int hr = rec.x & 255, hc = (rec.x >> 8) & 255, tr = (rec.x >> 16) & 255, tc = (rec.x >> 24) & 255;
     int dir = rec.y & 3, alive = (rec.y >> 8) & 1;
@@ -1274,12 +1277,12 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
 
     LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
-    if (isn) {
+    if (isn) {   // (steps/fruits/kills: the reference's msk * x sums, held as integers)
         const double msk = 1.0 - (double)dn;
         s0 = s0 + msk * rew;
-        s1 = s1 + msk * 1.0;
-        s2 = s2 + msk * (counted ? (double)eat : 0.0);
-        s3 = s3 + msk * (counted ? (double)kills : 0.0);
+        s1 += dn ? 0u : 1u;
+        s2 += (!dn && counted) ? (uint32_t)eat : 0u;
+        s3 += (!dn && counted) ? (uint32_t)kills : 0u;
     }
     if (isn) {   // an env rejected for an invalid action reports reward 0, not done
         o.rew[(int64_t)e * S + k] = live ? rew : 0.0;
@@ -1309,13 +1312,16 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     if (isn) {           // the episode summary where it ended, zeros elsewhere
         o.rank[(int64_t)e * S + k] = ep_end ? rank : 0;
         double *es = o.ep_stats + (int64_t)e * 4 * S;
-        es[k] = ep_end ? s0 : 0.0; es[S + k] = ep_end ? s1 : 0.0;
-        es[2 * S + k] = ep_end ? s2 : 0.0; es[3 * S + k] = ep_end ? s3 : 0.0;
+        es[k] = ep_end ? s0 : 0.0; es[S + k] = ep_end ? (double)s1 : 0.0;
+        es[2 * S + k] = ep_end ? (double)s2 : 0.0; es[3 * S + k] = ep_end ? (double)s3 : 0.0;
     }
-    if (ep_end) s0 = s1 = s2 = s3 = 0.0;                           // _reset_epi_stats
+    if (ep_end) { s0 = 0.0; s1 = s2 = s3 = 0u; }                   // _reset_epi_stats
     // a snake dead before this step keeps its statistics, record and (one frame)
     // crop centre: no stores for it
-    if (live && (counted || ep_end)) { sp[k] = s0; sp[S + k] = s1; sp[2 * S + k] = s2; sp[3 * S + k] = s3; }
+    if (live && (counted || ep_end)) {
+        const unsigned long long sb = (unsigned long long)__double_as_longlong(s0);
+        *sp = make_uint4((uint32_t)sb, (uint32_t)(sb >> 32), s1, (s2 & 0xffffu) | (s3 << 16));
+    }
 
     LSTAMP(46);
     // commit the new frames into their ring slots; records; crop centres

@@ -320,7 +320,7 @@ class SnakeVecEnv:
         er[i, 0] = int(alive_snakes)
         er[i, 1] = int(episode_length)
         er[i, 2] = fs - 1
-        self.stats.view(self.num_envs, 4 * S)[i].zero_()
+        self.stats.view(self.num_envs, -1)[i].zero_()
         self._reset_done = True
 
     def close(self):
