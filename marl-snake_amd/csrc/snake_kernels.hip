@@ -1438,9 +1438,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     const int T = R + P;
     if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
     // env of job j of queue q
-    auto job_env = [&](int q, int j, int qincl, int qcnt) {
-        const int sh = __ffsll((long long)__ballot(j >= qincl - qcnt && j < qincl)) - 1;
-        return st.resetq[(q * kQShards + sh) * c.q_cap + j - bcast(qincl - qcnt, sh)];
+    // (only the inclusive prefix sums stay live across the jobs: the shard of
+    // job j is the number of shards whose prefix ends at or before j)
+    auto job_env = [&](int q, int j, int qincl) {
+        const int sh = __popcll(__ballot(qincl <= j));
+        const int base = sh ? bcast(qincl, sh - 1) : 0;
+        return st.resetq[(q * kQShards + sh) * c.q_cap + j - base];
     };
     // job idx < R: the step's resets (high priority, the critical path); then
     // the urgent spawn-ahead jobs, then the others. A worker's first job is its
@@ -1451,7 +1454,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     for (;;) {
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
-            const int e = job_env(0, idx, incl, cnt);
+            const int e = job_env(0, idx, incl);
             WaveMT mt;
             const int spst = load_reset_mt(st, e, mt, lane);
             if (c.diag && lane == 0 && spst == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
@@ -1464,7 +1467,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             else if (c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(2);
             const int j = idx - R;
-            const int e = j < U ? job_env(1, j, uincl, ucnt) : job_env(2, j - U, nincl, ncnt);
+            const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
             if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
             if (j < 128) OBSPROF(512 + j, lane);
             if (c.link_in_lds) do_spawn<MS, true>(c, st, e, lds, blockIdx.x, lane);
