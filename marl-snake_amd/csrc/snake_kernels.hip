@@ -329,10 +329,35 @@ __device__ __forceinline__ void perm_record(int ii, int w, int S, NP *link, lu16
 // indices' offsets, and the draw record is written through a per-lane dummy
 // slot instead of exec masking: under the step's load the worker waves are
 // issue-bound, so instructions (SALU and branches included) are the cost.
+#ifndef SNAKE_DR_VPOPC
+#define SNAKE_DR_VPOPC 1
+#endif
+#ifndef SNAKE_DR_CLZ
+#define SNAKE_DR_CLZ 1
+#endif
+#ifndef SNAKE_DR_PAIRLOOP
+#define SNAKE_DR_PAIRLOOP 1
+#endif
+
+// population count of a wave mask on the vector ALU (`ones` is an opaque
+// all-ones VGPR): the scalar count of a mask a vector compare just wrote costs a
+// vector-to-scalar hand-off and a move back in the round's dependency chain
+__device__ __forceinline__ int vpopc(unsigned long long x, uint32_t ones)
+{
+#if SNAKE_DR_VPOPC
+    return __builtin_popcount((uint32_t)x & ones) + __builtin_popcount((uint32_t)(x >> 32) & ones);
+#else
+    (void)ones;
+    return __popcll(x);
+#endif
+}
+
+// Returns true when the round ended at a bracket cut inside the pair with
+// draws left: the next round reads the same register pair.
 template <typename NP>
-__device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base, WaveMT &m, int &i,
+__device__ __forceinline__ bool draw_round(uint32_t tw0, uint32_t tw1, int base, WaveMT &m, int &i,
                                            uint32_t &mask, int &lo, int S, NP *link, NP *dummy,
-                                           lu16 *jsmall, int lane)
+                                           lu16 *jsmall, uint32_t ones, int lane)
 {
     constexpr int kBig = 0x3fffffff;   // never accepted; w + b cannot overflow
     const int l0 = m.pos - base;
@@ -340,7 +365,7 @@ __device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base,
     const int w0 = p0 >= 0 ? (int)(tw0 & mask) : kBig;
     const int w1 = (p0 >= -64 && base + 64 + lane < kMtN) ? (int)(tw1 & mask) : kBig;
     unsigned long long c0 = __ballot(w0 <= i), c1 = __ballot(w1 <= i);
-    int b0 = mbcnt64(c0), b1 = mbcnt64(c1, __popcll(c0));
+    int b0 = mbcnt64(c0), b1 = mbcnt64(c1, vpopc(c0, ones));
     unsigned long long a0 = __ballot(w0 + b0 <= i), a1 = __ballot(w1 + b1 <= i);
     // (the empty asm keeps each test on the OR of both halves: folded into two
     // 64-bit compares it costs two selects and an AND per test)
@@ -369,7 +394,9 @@ __device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base,
     int A = A0 + __popcll(a1);
     int end = min(128, kMtN - base);
     const int k = i - lo + 1;  // accepts left in this bracket
+    bool cut = false;
     if (__builtin_expect(A >= k, 0)) {
+        cut = true;
         if (A0 >= k) {
             const int b = __ffsll((long long)__ballot(inv_ballot(a0) && b0 == k - 1)) - 1;
             a0 &= (2ull << b) - 1ull;
@@ -398,10 +425,17 @@ __device__ __forceinline__ void draw_round(uint32_t tw0, uint32_t tw1, int base,
     }
     m.pos = base + end;
     i -= A;
+#if SNAKE_DR_CLZ
+    // the bracket of the new i, branch-free (i < 1 ends the draws anyway)
+    mask = i > 0 ? (0xffffffffu >> __builtin_clz((uint32_t)i)) : 0u;
+    lo = (int)(mask >> 1) + 1;
+#else
     if (__builtin_expect(i < lo, 0)) {   // next power-of-two bracket (i < 1 ends the draws anyway)
         mask = gen_mask((uint32_t)i);
         lo = (int)(mask >> 1) + 1;
     }
+#endif
+    return cut && i >= 1 && end < 128 && m.pos < kMtN;
 }
 
 
@@ -421,6 +455,8 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
 #pragma unroll
     for (int t = 0; t < 10; t++) tk[t] = temper(m.w[t]);
     NP *dummy = link + link_n + lane;   // lanes with nothing to record hit their own dummy
+    uint32_t ones;
+    __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
     // every round advances the stream; the cap only guarantees that a broken
     // invariant ends the wave instead of hanging the GPU
     for (int guard = 0; i >= 1 && guard < (1 << 20); guard++) {
@@ -432,10 +468,23 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
         }
 #pragma unroll
         for (int q = 0; q < 5; q++) {
+#if SNAKE_DR_PAIRLOOP
+            // a round normally consumes the rest of the pair; only a bracket cut
+            // inside it repeats the pair
+            if (i >= 1 && m.pos < kMtN && (m.pos >> 7) == q) {
+                bool again;
+                do {
+                    COUNT(e, lane, 1);
+                    again = draw_round(tk[2 * q], tk[2 * q + 1], q << 7, m, i, mask, lo, S, link, dummy, jsmall,
+                                       ones, lane);
+                } while (__builtin_expect(again, 0));
+            }
+#else
             while (i >= 1 && m.pos < kMtN && (m.pos >> 7) == q) {
                 COUNT(e, lane, 1);
-                draw_round(tk[2 * q], tk[2 * q + 1], q << 7, m, i, mask, lo, S, link, dummy, jsmall, lane);
+                draw_round(tk[2 * q], tk[2 * q + 1], q << 7, m, i, mask, lo, S, link, dummy, jsmall, ones, lane);
             }
+#endif
         }
     }
     COUNT_FLUSH(e, lane);
