@@ -517,14 +517,22 @@ __device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int l
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
+            // one ballot against every tracked position (a move is rare: ~ln n
+            // per position over the whole scan); the per-position chase only
+            // when some lane matched
+            bool hit = false;
 #pragma unroll
-            for (int k = 0; k < MS; k++) {
-                if (k < S) {
-                    unsigned long long m = __ballot(jv[u] == xk[k]);
-                    while (m) {
-                        const int l = __ffsll((long long)m) - 1;
-                        xk[k] = base + u * kWave + l;
-                        m = __ballot(jv[u] == xk[k]);
+            for (int k = 0; k < MS; k++) hit |= (k < S) && jv[u] == xk[k];
+            if (__builtin_expect(__ballot(hit) != 0ull, 0)) {
+#pragma unroll
+                for (int k = 0; k < MS; k++) {
+                    if (k < S) {
+                        unsigned long long m = __ballot(jv[u] == xk[k]);
+                        while (m) {
+                            const int l = __ffsll((long long)m) - 1;
+                            xk[k] = base + u * kWave + l;
+                            m = __ballot(jv[u] == xk[k]);
+                        }
                     }
                 }
             }
@@ -1957,9 +1965,14 @@ __global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsi
     snake::mt_perm_draws(mt, n, S, jarr, n, jarr, lane);
     snake::wave_sync();
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    if (lane == 0) { out[0] = t1 - t0; out[1] = (unsigned long long)mt.pos; }
+    int q[4];
+    snake::perm_trace_j<4>(S, n, jarr, q, lane);
+    snake::wave_sync();
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { out[0] = t1 - t0; out[1] = (unsigned long long)mt.pos; out[2] = t2 - t1; out[3] = (unsigned long long)q[0]; }
 }
 
+// out_dev: [draw cycles, final MT position, trace cycles, arr[0]]
 extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, int S, unsigned long long *out_dev)
 {
     hipLaunchKernelGGL(k_drawbench, dim3(1), dim3(64), 2 * n + 256, 0, mt_dev, pos0, n, S, out_dev);

@@ -17,11 +17,13 @@ L = _native.lib(path)
 L.snake_debug_drawbench.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 v = SnakeVecEnv(64, num_snakes=4, seed=0, lib_path=path, height=20, width=20, vision_range=5)
 v.reset()
-out = torch.zeros(2, dtype=torch.int64, device='cuda')
-res = []
+out = torch.zeros(4, dtype=torch.int64, device='cuda')
+res, tr = [], []
 for e in range(16):
     mt = v.mt.view(64, 624)[e]
     for rep in range(3):
         L.snake_debug_drawbench(mt.data_ptr(), 624, v.layout.n_cand, 4, out.data_ptr())
         res.append(int(out[0]))
-print(json.dumps({'lib': os.path.basename(path), 'n_cand': v.layout.n_cand, 'cycles_min': min(res), 'cycles_median': sorted(res)[len(res) // 2]}))
+        tr.append(int(out[2]))
+print(json.dumps({'lib': os.path.basename(path), 'n_cand': v.layout.n_cand, 'cycles_min': min(res), 'cycles_median': sorted(res)[len(res) // 2],
+                  'trace_cycles_median': sorted(tr)[len(tr) // 2]}))
