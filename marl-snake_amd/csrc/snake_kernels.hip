@@ -496,6 +496,10 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
 // when j_i == x (the swap brings arr[i] there; x < i always). Every tracked
 // position is tested against a chunk with one ballot; a hit re-tests the rest
 // of the chunk from the new position.
+#ifndef SNAKE_TRACE_DIST
+#define SNAKE_TRACE_DIST 1
+#endif
+
 template <int MS>
 __device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int lane)
 {
@@ -504,9 +508,12 @@ __device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int l
         const int j = jarr[i];
         x = (x == i) ? j : (x == j ? i : x);
     }
-    int xk[MS];
+    int xk[MS], xt[MS];
 #pragma unroll
-    for (int k = 0; k < MS; k++) xk[k] = bcast(x, k);
+    for (int k = 0; k < MS; k++) {
+        xk[k] = bcast(x, k);
+        xt[k] = k < S ? xk[k] : 0x7fffffff;   // (record entries are < 65 536 or -1)
+    }
     for (int base = S; base < n; base += 4 * kWave) {
         int jv[4];
 #pragma unroll
@@ -520,9 +527,21 @@ __device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int l
             // one ballot against every tracked position (a move is rare: ~ln n
             // per position over the whole scan); the per-position chase only
             // when some lane matched
+#if SNAKE_TRACE_DIST
+            // (the distance to the nearest tracked position, all on the vector
+            // ALU: one vector-to-scalar hand-off per block)
+            uint32_t dmin = 0xffffffffu;
+#pragma unroll
+            for (int k = 0; k < MS; k++) {
+                const uint32_t a = (uint32_t)jv[u], b = (uint32_t)xt[k];
+                dmin = min(dmin, max(a, b) - min(a, b));
+            }
+            const bool hit = dmin == 0u;
+#else
             bool hit = false;
 #pragma unroll
             for (int k = 0; k < MS; k++) hit |= (k < S) && jv[u] == xk[k];
+#endif
             if (__builtin_expect(__ballot(hit) != 0ull, 0)) {
 #pragma unroll
                 for (int k = 0; k < MS; k++) {
@@ -533,6 +552,7 @@ __device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int l
                             xk[k] = base + u * kWave + l;
                             m = __ballot(jv[u] == xk[k]);
                         }
+                        xt[k] = xk[k];
                     }
                 }
             }

@@ -15,7 +15,8 @@ from marlenv import SnakeVecEnv, _native  # noqa: E402
 path = os.path.abspath(sys.argv[1])
 L = _native.lib(path)
 L.snake_debug_drawbench.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
-v = SnakeVecEnv(64, num_snakes=4, seed=0, lib_path=path, height=20, width=20, vision_range=5)
+hw = int(sys.argv[2]) if len(sys.argv) > 2 else 20   # board size (40: cfg5's 16 424 poses)
+v = SnakeVecEnv(64, num_snakes=4, seed=0, lib_path=path, height=hw, width=hw, vision_range=5)
 v.reset()
 out = torch.zeros(4, dtype=torch.int64, device='cuda')
 res, tr = [], []
