@@ -496,10 +496,6 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
 // when j_i == x (the swap brings arr[i] there; x < i always). Every tracked
 // position is tested against a chunk with one ballot; a hit re-tests the rest
 // of the chunk from the new position.
-#ifndef SNAKE_TRACE_DIST
-#define SNAKE_TRACE_DIST 1
-#endif
-
 template <int MS>
 __device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int lane)
 {
@@ -508,40 +504,46 @@ __device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int l
         const int j = jarr[i];
         x = (x == i) ? j : (x == j ? i : x);
     }
-    int xk[MS], xt[MS];
+    // tracked positions, and as packed 16-bit pairs for the match test
+    // (positions and record entries are < 65 535; untracked slots and the
+    // padding past n are 0xffff: a padding match only sends the last chunk down
+    // the exact per-position path)
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    int xk[MS];
+    u16x2 xp[MS / 2];
 #pragma unroll
-    for (int k = 0; k < MS; k++) {
-        xk[k] = bcast(x, k);
-        xt[k] = k < S ? xk[k] : 0x7fffffff;   // (record entries are < 65 536 or -1)
-    }
+    for (int k = 0; k < MS; k++) xk[k] = bcast(x, k);
+    auto pack = [&]() {
+#pragma unroll
+        for (int p2 = 0; p2 < MS / 2; p2++) {
+            xp[p2].x = (unsigned short)(2 * p2 < S ? xk[2 * p2] : 0xffff);
+            xp[p2].y = (unsigned short)(2 * p2 + 1 < S ? xk[2 * p2 + 1] : 0xffff);
+        }
+    };
+    pack();
     for (int base = S; base < n; base += 4 * kWave) {
         int jv[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int i = base + u * kWave + lane;
             jv[u] = (int)jarr[min(i, n - 1)];
-            jv[u] = i < n ? jv[u] : -1;
+            jv[u] = i < n ? jv[u] : 0xffff;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             // one ballot against every tracked position (a move is rare: ~ln n
             // per position over the whole scan); the per-position chase only
             // when some lane matched
-#if SNAKE_TRACE_DIST
-            // (the distance to the nearest tracked position, all on the vector
-            // ALU: one vector-to-scalar hand-off per block)
-            uint32_t dmin = 0xffffffffu;
+            // (packed 16-bit differences to two tracked positions per vector
+            // instruction, their minimum; zero = a match: one vector-to-scalar
+            // hand-off per block)
+            u16x2 jj;
+            jj.x = (unsigned short)jv[u];
+            jj.y = (unsigned short)jv[u];
+            u16x2 dm = jj - xp[0];
 #pragma unroll
-            for (int k = 0; k < MS; k++) {
-                const uint32_t a = (uint32_t)jv[u], b = (uint32_t)xt[k];
-                dmin = min(dmin, max(a, b) - min(a, b));
-            }
-            const bool hit = dmin == 0u;
-#else
-            bool hit = false;
-#pragma unroll
-            for (int k = 0; k < MS; k++) hit |= (k < S) && jv[u] == xk[k];
-#endif
+            for (int p2 = 1; p2 < MS / 2; p2++) dm = __builtin_elementwise_min(dm, jj - xp[p2]);
+            const bool hit = min(dm.x, dm.y) == 0;
             if (__builtin_expect(__ballot(hit) != 0ull, 0)) {
 #pragma unroll
                 for (int k = 0; k < MS; k++) {
@@ -552,9 +554,9 @@ __device__ void perm_trace_j(int S, int n, const lu16 *jarr, int (&q)[MS], int l
                             xk[k] = base + u * kWave + l;
                             m = __ballot(jv[u] == xk[k]);
                         }
-                        xt[k] = xk[k];
                     }
                 }
+                pack();
             }
         }
     }
