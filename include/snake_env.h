@@ -251,7 +251,7 @@ int snake_dqn_forward(const snake_dqn_cfg *cfg, const snake_dqn_net *net, const 
                       void *stream);
 
 /* fp32 mode of the DQN consumer (dqn32_kernels.hip): the same network in fp32
- * arithmetic on any observation size (e.g. train_dqn.py's 20x20 full map,
+ * arithmetic (fp32 matrix cores: exact fp32 products, fp32 sums) on any observation size (e.g. train_dqn.py's 20x20 full map,
  * :29-33), cfg->channels a multiple of 8, conv_waves ignored. Weights fp32,
  * row-major [out][in]: conv w [cout][9*cin] with k = (ky*3 + kx)*cin + ci;
  * fc1 [256][h*w*64] with column p*64 + ch (the reference's NCHW flatten
