@@ -164,10 +164,12 @@ def _obs_full(B, fs=1, S=4, seed=0, H=20, W=20):
 @pytest.mark.gpu
 @pytest.mark.parametrize('B,shape,full', [(64, (20, 20, 8), True), (37, (20, 20, 16), True), (1, (20, 20, 8), True),
                                           (300, (11, 11, 8), False), (50, (11, 11, 32), False),
-                                          (20, (12, 10, 8), True)])
+                                          (20, (12, 10, 8), True), (3, (48, 48, 8), True)])
 def test_dqn_fp32_matches_reference(B, shape, full):
     """precision='fp32' against the reference network in float64 on the CPU,
-    |err| <= 1e-5 * max|q| (train_dqn.py's own Config: 20x20x8 full map)."""
+    |err| <= 1e-5 * max|q| (train_dqn.py's own Config: 20x20x8 full map). The
+    48x48 map is wider than the matrix-core convolutions' LDS patch holds: its
+    convolutions take the vector-ALU GEMM (dqn32_kernels.hip)."""
     from marlenv.dqn import DQNForward
     h, w, c = shape
     torch.manual_seed(2)
