@@ -148,6 +148,15 @@ def main():
     ap.add_argument('--frame-stack', type=int, default=None)
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--dist-backend', choices=('nccl', 'gloo'), default='nccl',
+                    help='process group of the timing barrier / max-reduce (gloo: CPU tensors; '
+                         'lets several ranks share one GPU, e.g. the two-rank test on a one-GPU box)')
+    ap.add_argument('--global-actions', action='store_true',
+                    help="every rank draws the WHOLE batch's actions and takes its shard's rows, so "
+                         'any world size replays the same rollout (check runs; the default draws per rank)')
+    ap.add_argument('--dump-dir', default=None,
+                    help='write rank<r>.npz with the shard range, final grids, MT keys/positions, '
+                         'env records, the last step\'s obs and each env\'s summed rewards')
     ap.add_argument('--timing-stride', type=int, default=8,
                     help='bracket the kernels of every k-th timed step with timing events '
                          '(0: none; the events cost ~12 us per timed step)')
@@ -176,11 +185,16 @@ def main():
         if world == 1 and args.gpus > 1:
             sys.exit('--gpus N>1 needs one process per GPU: launch with torch.distributed.run')
     distributed = world > 1
+    ordinal = local_rank % max(1, torch.cuda.device_count())   # ranks beyond the GPUs share them (gloo only)
     if distributed:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
-    device = torch.device('cuda', local_rank if distributed else torch.cuda.current_device())
+        torch.cuda.set_device(ordinal)
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', ordinal))
+        else:
+            dist.init_process_group('gloo')
+    device = torch.device('cuda', ordinal if distributed else torch.cuda.current_device())
+    red_device = device if args.dist_backend == 'nccl' else torch.device('cpu')
 
     from marlenv import SnakeVecEnv
     from marlenv import _native
@@ -191,12 +205,20 @@ def main():
     venv = SnakeVecEnv(hi - lo, num_snakes=S, device=device, seed=0, env_offset=lo, **env_kw)
     venv.reset()
     gen = torch.Generator(device=device)
-    gen.manual_seed(12345 + rank)
     n_act = args.warmup + args.steps
-    actions = torch.randint(0, 3, (n_act, hi - lo, S), generator=gen, device=device, dtype=torch.int8)
+    if args.global_actions:
+        gen.manual_seed(12345)
+        actions = torch.randint(0, 3, (n_act, n_total, S), generator=gen, device=device,
+                                dtype=torch.int8)[:, lo:hi].contiguous()
+    else:
+        gen.manual_seed(12345 + rank)
+        actions = torch.randint(0, 3, (n_act, hi - lo, S), generator=gen, device=device, dtype=torch.int8)
+    rsum = torch.zeros((hi - lo, S), dtype=torch.float64, device=device) if args.dump_dir else None
 
     for t in range(args.warmup):
-        venv.step(actions[t])
+        out = venv.step(actions[t])
+        if rsum is not None:
+            rsum += out[1]
     torch.cuda.synchronize(device)
 
     L = _native.lib()
@@ -211,7 +233,9 @@ def main():
         timed = stride > 0 and t % stride == 0
         if timed:
             _native.timing_enable(True, L)
-        venv.step(actions[args.warmup + t])
+        out = venv.step(actions[args.warmup + t])
+        if rsum is not None:
+            rsum += out[1]
         if timed:
             _native.timing_enable(False, L)
     torch.cuda.synchronize(device)
@@ -229,7 +253,7 @@ def main():
     sp_hits = _native.timing_read('spawn_hits', L)[1]
     sp_jobs = _native.timing_read('spawn_jobs', L)[1]
 
-    red = reduce_max([elapsed] + list(kern.values()), device, dist if distributed else None)
+    red = reduce_max([elapsed] + list(kern.values()), red_device, dist if distributed else None)
     elapsed, kern = red[0], dict(zip(kern, red[1:]))
 
     lay = venv.layout
@@ -279,6 +303,14 @@ def main():
         'cpu_baseline': None,
     }
     line['cpu_baseline'] = cpu
+    if args.dump_dir:
+        import numpy as np
+        os.makedirs(args.dump_dir, exist_ok=True)
+        keys, pos = venv.mt_state()
+        np.savez(os.path.join(args.dump_dir, f'rank{rank}.npz'), lo=lo, hi=hi, world=world,
+                 grids=venv.grids().cpu().numpy(), mt=keys.cpu().numpy(), mt_pos=pos.cpu().numpy(),
+                 env=venv.env_rec.view(hi - lo, 8).cpu().numpy(), obs=out[0].cpu().numpy(),
+                 rew_sum=rsum.cpu().numpy())
     if rank == 0:
         print(json.dumps(line), flush=True)
     if distributed:

@@ -6,6 +6,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <math.h>
+
 #include <algorithm>
 #include <map>
 #include <mutex>
@@ -167,7 +169,7 @@ static int64_t build_table(int H, int W, int L, std::vector<int16_t> *out)
 struct PoseTable {
     int64_t n = 0;
     std::vector<int16_t> cells;
-    std::map<int, double> p_disjoint;
+    std::map<int, std::pair<double, int64_t>> p_disjoint;   // S -> (estimate, samples)
 };
 
 static std::mutex g_table_mu;
@@ -191,14 +193,18 @@ static int64_t cached_count(int H, int W, int L)
 
 // Monte-Carlo estimate (fixed seed, so deterministic) of P(S uniformly drawn
 // distinct poses share no cell): up to 2e5 samples, stopping once 400 disjoint
-// draws have been seen.
-static double disjoint_prob(int H, int W, int L, int S)
+// draws have been seen. *samples = the draws the estimate rests on.
+static double disjoint_prob(int H, int W, int L, int S, int64_t *samples)
 {
     std::lock_guard<std::mutex> lock(g_table_mu);
     PoseTable &t = pose_table(H, W, L);
     auto it = t.p_disjoint.find(S);
-    if (it != t.p_disjoint.end()) return it->second;
+    if (it != t.p_disjoint.end()) {
+        *samples = it->second.second;
+        return it->second.first;
+    }
     double p = 1.0;
+    int64_t drawn = 0;
     if (S > 1 && t.n >= S) {
         std::vector<uint32_t> stamp((size_t)H * W, 0u);
         uint64_t x = 0x9e3779b97f4a7c15ull;
@@ -227,9 +233,11 @@ static double disjoint_prob(int H, int W, int L, int S)
             }
             hits += ok;
         }
-        p = (double)hits / (double)(m - 1);
+        drawn = m - 1;
+        p = (double)hits / (double)drawn;
     }
-    t.p_disjoint[S] = p;
+    t.p_disjoint[S] = std::make_pair(p, drawn);
+    *samples = drawn;
     return p;
 }
 
@@ -293,11 +301,14 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
         set_error("only %lld spawn poses for %lld snakes", (long long)o->n_cand, (long long)S);
         return SNAKE_E_CONFIG;
     }
-    const double pd = disjoint_prob(c->height, c->width, c->snake_length, (int)S);
+    int64_t samples = 0;
+    const double pd = disjoint_prob(c->height, c->width, c->snake_length, (int)S, &samples);
     if (pd < kMinDisjoint) {
         set_error("%dx%d board too crowded: %lld snakes of length %d are disjoint in only "
-                  "%.2g of the spawn draws (the reference would retry ~%.0f permutations per reset)",
-                  c->height, c->width, (long long)S, c->snake_length, pd, pd > 0 ? 1.0 / pd : 1e30);
+                  "%.2g of the spawn draws (Monte-Carlo estimate: %lld of %lld sampled draws; the limit is %.0e; "
+                  "the reference would retry ~%.0f permutations per reset)",
+                  c->height, c->width, (long long)S, c->snake_length, pd, (long long)llround(pd * samples),
+                  (long long)samples, kMinDisjoint, pd > 0 ? 1.0 / pd : 1e30);
         return SNAKE_E_CONFIG;
     }
     return SNAKE_OK;
@@ -435,6 +446,37 @@ static int64_t n_cand_of(const snake_cfg *c)
     return lay.n_cand;
 }
 
+// build_kcfg of the step/reset/seed calls, memoised per thread: the plan is a
+// pure function of (cfg, num_envs) (the environment knobs are read once), and
+// re-planning on every snake_step cost host time on the step's critical path
+// at small N (layout_of twice, two mutex-guarded table lookups).
+static int plan_cached(const snake_cfg *c, int64_t N, KCfg *k)
+{
+    struct Entry {
+        snake_cfg cfg;
+        int64_t n;
+        KCfg k;
+    };
+    thread_local Entry memo[8];
+    thread_local int used = 0, next = 0;
+    if (!c) { set_error("cfg is NULL"); return SNAKE_E_CONFIG; }
+    for (int i = 0; i < used; i++) {
+        if (memo[i].n == N && memcmp(&memo[i].cfg, c, sizeof *c) == 0) {
+            *k = memo[i].k;
+            return SNAKE_OK;
+        }
+    }
+    int rc = build_kcfg(c, N, n_cand_of(c), k);
+    if (rc) return rc;
+    Entry &e = memo[next];
+    e.cfg = *c;
+    e.n = N;
+    e.k = *k;
+    next = (next + 1) % 8;
+    used = used < 8 ? used + 1 : 8;
+    return SNAKE_OK;
+}
+
 }  // namespace snake
 
 using namespace snake;
@@ -472,7 +514,7 @@ int snake_seed(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, ui
                int64_t env_offset, void *stream)
 {
     KCfg k;
-    int rc = build_kcfg(cfg, num_envs, n_cand_of(cfg), &k);
+    int rc = plan_cached(cfg, num_envs, &k);
     if (rc) return rc;
     if ((rc = check_state(k, st, false))) return rc;
     if (env_offset < 0) { set_error("env_offset < 0"); return SNAKE_E_ARG; }
@@ -483,7 +525,7 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
                 const uint8_t *env_mask, const snake_out *out, void *stream)
 {
     KCfg k;
-    int rc = build_kcfg(cfg, num_envs, n_cand_of(cfg), &k);
+    int rc = plan_cached(cfg, num_envs, &k);
     if (rc) return rc;
     if ((rc = check_state(k, st, true))) return rc;
     if ((rc = check_out(out, false))) return rc;
@@ -494,7 +536,7 @@ int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, co
                const snake_out *out, void *stream)
 {
     KCfg k;
-    int rc = build_kcfg(cfg, num_envs, n_cand_of(cfg), &k);
+    int rc = plan_cached(cfg, num_envs, &k);
     if (rc) return rc;
     if ((rc = check_state(k, st, true))) return rc;
     if ((rc = check_out(out, true))) return rc;
@@ -506,7 +548,7 @@ int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_en
                      const uint8_t *palette, uint8_t *rgb, void *stream)
 {
     KCfg k;
-    int rc = build_kcfg(cfg, num_envs, n_cand_of(cfg), &k);
+    int rc = plan_cached(cfg, num_envs, &k);
     if (rc) return rc;
     if (!st || !st->grid || !st->env) { set_error("snake_state.grid/env is NULL"); return SNAKE_E_ARG; }
     if (!palette) { set_error("palette is NULL"); return SNAKE_E_ARG; }

@@ -1096,8 +1096,10 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const uint32_t all_m = (1u << S) - 1u;
     const bool ep_end = !bad && (c.coop ? (done_m != 0u) : (done_m == all_m));
     if (c.coop && ep_end) fd = 1;
-    // (autoreset 2: every env, gym 0.23.1's reset after every step)
-    const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && !bad && (ep_end || c.autoreset == 2))
+    // (autoreset 2: every env, gym 0.23.1's reset after every step; an env
+    // rejected for an invalid action is queued too, for an encode of its
+    // unchanged state: no k_encode runs in that mode)
+    const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && (c.autoreset == 2 || (!bad && ep_end)))
                                               : 0ull;
     const int shard = blockIdx.x % kQShards;
     int qbase = 0;
@@ -1496,6 +1498,25 @@ __device__ void spawn_after_reset(const KCfg &c, const snake_state &st, int e, W
 // many registers, link table in LDS) and then the queued spawn-ahead jobs,
 // k_encode encodes every other env's stacked frames (bandwidth-bound, few
 // registers: full occupancy).
+// The observation of env e's current frame stack (_get_obs, snake_env.py:461-472):
+// the grid ring and crop centres staged in LDS, then the (staged) encode.
+__device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st, const snake_out &o, int e,
+                                           uint8_t *lds, int lane)
+{
+    const int fs = c.fs, S = c.S;
+    uint8_t *frames = lds + c.lds_frames;
+    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
+    const int cur = st.env[(int64_t)e * kEnvRec + ENV_CUR];
+    stage_to_lds(frames, st.grid + (int64_t)e * c.ring_bytes, c.ring_bytes, lane);
+    for (int q = lane; q < fs * S; q += kWave) {
+        const int x = q / S, k = q - x * S;
+        const int p = st.ctr[(int64_t)e * fs * S + q];
+        org[x * kMaxSnakes + k] = pack_origin(c, p >> 8, p & 255);
+    }
+    wave_sync();
+    encode_obs(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lds, lane);
+}
+
 template <int MS>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KCfg c, const snake_state st, const snake_out o)
 {
@@ -1508,7 +1529,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
               ncnt = qc[(2 * kQShards + lane) * kQSpread];
     const int incl = wave_scan(cnt, lane), uincl = wave_scan(ucnt, lane), nincl = wave_scan(ncnt, lane);
     const int R = bcast(incl, kWave - 1), U = bcast(uincl, kWave - 1);
-    const int G = (int)gridDim.x, x = blockIdx.x % kClaimShards;
+    // claim shards: min(G, kClaimShards), so that every shard has a worker
+    const int G = (int)gridDim.x, nsh = min(G, kClaimShards), x = blockIdx.x % nsh;
     // spawn_cap: the other (2-live-snake) jobs only as far as the first round
     // of workers reaches; their envs are queued again next step
     int Nn = bcast(nincl, kWave - 1);
@@ -1534,13 +1556,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
             const int e = job_env(0, idx, incl);
-            WaveMT mt;
-            const int spst = load_reset_mt(st, e, mt, lane);
-            if (c.diag && lane == 0 && spst == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
-            if (idx < 128) OBSPROF(idx, lane);
-            if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
-            else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
-            if (idx < 128) OBSPROF(128 + idx, lane);
+            if (c.autoreset == 2 && o.err[e] == 1) {
+                // every-step mode, an env rejected for an invalid action: left
+                // unchanged (the reference raises before touching it), so its
+                // observation is the encode of its current frames
+                encode_env(c, st, o, e, lds, lane);
+            } else {
+                WaveMT mt;
+                const int spst = load_reset_mt(st, e, mt, lane);
+                if (c.diag && lane == 0 && spst == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
+                if (idx < 128) OBSPROF(idx, lane);
+                if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
+                else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
+                if (idx < 128) OBSPROF(128 + idx, lane);
+            }
         } else if (idx < R + P) {
             if (c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
             else if (c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -1556,7 +1585,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         int v = 0;
         if (lane == 0) v = atomicAdd(&qc[(kQClaim + x) * kQSpread], 1);
         nx = bcast(v, 0);
-        idx = G + x + kClaimShards * nx;
+        idx = G + x + nsh * nx;
         if (idx >= T) break;
     }
     // Every worker ends with exactly one failing claim, so the shard's claims
@@ -1565,12 +1594,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     // step's counters for the next step: every worker has read its counts and
     // made its last claim by then (no host-side step parity, one extra atomic
     // per shard).
-    const int jobs_x = T > G + x ? (T - G - x + kClaimShards - 1) / kClaimShards : 0;
-    const int workers_x = (G - x + kClaimShards - 1) / kClaimShards;
+    const int jobs_x = T > G + x ? (T - G - x + nsh - 1) / nsh : 0;
+    const int workers_x = (G - x + nsh - 1) / nsh;
     if (nx == jobs_x + workers_x - 1) {
         int d = 0;
         if (lane == 0) d = atomicAdd(&qc[kQDone * kQSpread], 1);
-        if (bcast(d, 0) == min(G, kClaimShards) - 1)
+        if (bcast(d, 0) == nsh - 1)
             for (int q = lane; q < kQCount; q += kWave) qc[q * kQSpread] = 0;
     }
 }
@@ -1586,18 +1615,7 @@ __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state s
     if (c.encode_prio == 1) __builtin_amdgcn_s_setprio(1);      // (setprio takes an immediate)
     else if (c.encode_prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (c.encode_prio == 3) __builtin_amdgcn_s_setprio(3);
-    const int fs = c.fs, S = c.S;
-    uint8_t *frames = lds + c.lds_frames;
-    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
-    const int cur = st.env[(int64_t)e * kEnvRec + ENV_CUR];
-    stage_to_lds(frames, st.grid + (int64_t)e * c.ring_bytes, c.ring_bytes, lane);
-    for (int q = lane; q < fs * S; q += kWave) {
-        const int x = q / S, k = q - x * S;
-        const int p = st.ctr[(int64_t)e * fs * S + q];
-        org[x * kMaxSnakes + k] = pack_origin(c, p >> 8, p & 255);
-    }
-    wave_sync();
-    encode_obs(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lds, lane);
+    encode_env(c, st, o, e, lds, lane);
     if (prof_) OBSPROF(384 + (e >> 9), lane);
 }
 

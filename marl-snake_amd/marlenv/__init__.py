@@ -8,7 +8,7 @@ tranthai189765/MARL-Snake, stepped by hand-written HIP kernels on CDNA4.
 from .envs import CoopSnakeEnv, SnakeEnv  # noqa: F401
 from .vec_env import SnakeVecEnv  # noqa: F401
 from .dqn import DQNForward  # noqa: F401
-from .wrappers import RenderGUI, SingleAgent, SingleMultiAgent, make_snake  # noqa: F401
+from .wrappers import RenderGUI, SingleAgent, SingleAgentVec, SingleMultiAgent, make_snake  # noqa: F401
 
 __version__ = '0.1.0'
 

@@ -25,6 +25,24 @@ def _torch():
     return torch
 
 
+# The reference network's parameter shapes (train_dqn.py:104-151): the kernels
+# hard-code 32/64/64 conv channels and 256/128 fc widths, so a mismatched state
+# dict must raise here instead of making them read past the packed weights.
+def _check_shapes(state, C, P, A):
+    want = {'conv1.weight': (32, C, 3, 3), 'conv1.bias': (32,),
+            'conv2.weight': (64, 32, 3, 3), 'conv2.bias': (64,),
+            'conv3.weight': (64, 64, 3, 3), 'conv3.bias': (64,),
+            'fc1.weight': (256, 64 * P), 'fc1.bias': (256,),
+            'fc2.weight': (128, 256), 'fc2.bias': (128,),
+            'fc3.weight': (A, 128), 'fc3.bias': (A,)}
+    for name, shape in want.items():
+        if name not in state:
+            raise ValueError('state dict has no %s' % name)
+        got = tuple(state[name].shape)
+        if got != shape:
+            raise ValueError('%s shape %s != %s' % (name, got, shape))
+
+
 class DQNForward:
     """DQN(input_shape=(N, h, w, c), num_actions) forward on uint8 NHWC observations.
 
@@ -47,6 +65,7 @@ class DQNForward:
         self.precision = precision
         self.num_actions = int(num_actions)
         self._scratch = None
+        _check_shapes(state, int(channels), int(height) * int(width), int(num_actions))
         if precision == 'fp32':
             self._init_fp32(state)
             return

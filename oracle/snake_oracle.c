@@ -750,3 +750,135 @@ done:
     free(obs);
     return n;
 }
+
+/* ---- batch checker (tests/test_gpu_parity.py full-size cases) ------------
+ * n envs seeded seed+i, every env stepped with its own actions and reset when
+ * its episode ends (all dones; any under coop), the vector-env auto-reset
+ * (wrappers.py:141-143): the reset obs replaces the step's, rewards/dones and the
+ * episode summary stay the step's. Envs are split over nthreads pthreads. */
+#include <pthread.h>
+
+struct so_batch {
+    so_cfg cfg;
+    int64_t n, obs_sz;
+    so_env **envs;
+};
+
+so_batch *so_batch_create(const so_cfg *cfg, int64_t n, uint32_t seed)
+{
+    if (n < 1) return NULL;
+    so_batch *b = (so_batch *)calloc(1, sizeof *b);
+    if (!b) return NULL;
+    b->cfg = *cfg;
+    b->n = n;
+    b->envs = (so_env **)calloc((size_t)n, sizeof *b->envs);
+    if (!b->envs) { free(b); return NULL; }
+    for (int64_t i = 0; i < n; i++) {
+        if (!(b->envs[i] = so_create(cfg, seed + (uint32_t)i))) { so_batch_destroy(b); return NULL; }
+    }
+    b->obs_sz = so_obs_size(b->envs[0]);
+    return b;
+}
+
+void so_batch_destroy(so_batch *b)
+{
+    if (!b) return;
+    if (b->envs)
+        for (int64_t i = 0; i < b->n; i++) if (b->envs[i]) so_destroy(b->envs[i]);
+    free(b->envs);
+    free(b);
+}
+
+typedef struct {
+    so_batch *b;
+    int64_t lo, hi;
+    const int8_t *actions;      /* NULL: reset */
+    uint8_t *obs, *dones, *ep_done;
+    double *rews, *ep_stats;    /* ep_stats [n][4][S] */
+    int32_t *rank, *err;
+} so_batch_job;
+
+static void *so_batch_run(void *arg)
+{
+    so_batch_job *j = (so_batch_job *)arg;
+    const int S = j->b->cfg.num_snakes;
+    for (int64_t i = j->lo; i < j->hi; i++) {
+        so_env *e = j->b->envs[i];
+        uint8_t *obs = j->obs + i * j->b->obs_sz;
+        if (!j->actions) { so_reset(e, obs); continue; }
+        int32_t a[16];
+        for (int k = 0; k < S; k++) a[k] = j->actions[i * S + k];
+        so_info info;
+        memset(&info, 0, sizeof info);
+        double *rw = j->rews + i * S;
+        uint8_t *dn = j->dones + i * S;
+        int32_t *rk = j->rank + i * S;
+        double *es = j->ep_stats + i * 4 * S;
+        int dir0[16];
+        for (int k = 0; k < S; k++) dir0[k] = e->snakes[k].dir;
+        const int rc = so_step(e, a, obs, rw, dn, &info);
+        /* the reference turns the snakes before the invalid one, then raises;
+         * the batch env (snake_env.h) leaves a rejected env entirely unchanged */
+        if (rc < 0)
+            for (int k = 0; k < S; k++) e->snakes[k].dir = dir0[k];
+        j->ep_done[i] = rc == 1;
+        j->err[i] = rc < 0;
+        for (int k = 0; k < S; k++) {
+            if (rc < 0) { rw[k] = 0.0; dn[k] = 0; }
+            rk[k] = rc == 1 ? (int32_t)info.rank[k] : 0;
+            es[k] = rc == 1 ? info.scores[k] : 0.0;
+            es[S + k] = rc == 1 ? info.steps[k] : 0.0;
+            es[2 * S + k] = rc == 1 ? info.fruits[k] : 0.0;
+            es[3 * S + k] = rc == 1 ? info.kills[k] : 0.0;
+        }
+        if (rc < 0) emit_obs(e, obs);   /* rejected: the unchanged state's obs */
+        if (rc == 1) so_reset(e, obs);
+    }
+    return NULL;
+}
+
+static int so_batch_launch(so_batch_job *proto, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    pthread_t th[64];
+    so_batch_job jobs[64];
+    const int64_t n = proto->b->n, per = (n + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = *proto;
+        jobs[t].lo = t * per < n ? t * per : n;
+        jobs[t].hi = (t + 1) * per < n ? (t + 1) * per : n;
+        if (t == 0) continue;
+        if (pthread_create(&th[t], NULL, so_batch_run, &jobs[t]) != 0) {
+            so_batch_run(&jobs[t]);   /* no thread: run it here */
+            th[t] = 0;
+        }
+    }
+    so_batch_run(&jobs[0]);
+    for (int t = 1; t < nthreads; t++) if (th[t]) pthread_join(th[t], NULL);
+    return 0;
+}
+
+int so_batch_reset(so_batch *b, uint8_t *obs, int nthreads)
+{
+    so_batch_job j;
+    memset(&j, 0, sizeof j);
+    j.b = b; j.obs = obs;
+    return so_batch_launch(&j, nthreads);
+}
+
+int so_batch_step(so_batch *b, const int8_t *actions, uint8_t *obs, double *rews, uint8_t *dones,
+                  uint8_t *ep_done, int32_t *rank, double *ep_stats, int32_t *err, int nthreads)
+{
+    so_batch_job j;
+    memset(&j, 0, sizeof j);
+    j.b = b; j.actions = actions; j.obs = obs; j.rews = rews; j.dones = dones; j.ep_done = ep_done;
+    j.rank = rank; j.ep_stats = ep_stats; j.err = err;
+    return so_batch_launch(&j, nthreads);
+}
+
+void so_batch_grids(const so_batch *b, uint8_t *out)
+{
+    const int64_t hw = (int64_t)b->cfg.height * b->cfg.width;
+    for (int64_t i = 0; i < b->n; i++) so_get_grid(b->envs[i], out + i * hw);
+}

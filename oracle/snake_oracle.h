@@ -65,6 +65,19 @@ int     so_inject(so_env *e, const int32_t *grid, const int32_t *coords, const i
  * actions, all-done resets; returns env-steps run (-1 on error). */
 int64_t so_rollout(const so_cfg *cfg, int32_t n_env, uint32_t seed, int64_t steps, uint32_t act_seed);
 
+/* ---- batch checker: n envs seeded seed..seed+n-1, stepped on nthreads threads
+ * with the vector env's all-done (coop: any-done) auto-reset -- the reset obs
+ * replaces the step's; rank / ep_stats [n][4][S] are the episode summary where
+ * ep_done, zeros elsewhere; an invalid action (err 1) leaves the env unchanged
+ * with reward 0, done 0 and its unchanged obs (snake_env.h snake_step). */
+typedef struct so_batch so_batch;
+so_batch *so_batch_create(const so_cfg *cfg, int64_t n, uint32_t seed);
+void    so_batch_destroy(so_batch *b);
+int     so_batch_reset(so_batch *b, uint8_t *obs, int nthreads);
+int     so_batch_step(so_batch *b, const int8_t *actions, uint8_t *obs, double *rews, uint8_t *dones,
+                      uint8_t *ep_done, int32_t *rank, double *ep_stats, int32_t *err, int nthreads);
+void    so_batch_grids(const so_batch *b, uint8_t *out);   /* [n][H*W] */
+
 /* ---- RNG / tables (checked against tests/golden/rng.npz, candidates.npz) -- */
 void    so_rng_raw(uint32_t seed, int64_t n, uint32_t *out);
 /* randint(0, n, size=k) after seed(seed); *next = the following raw draw */

@@ -71,6 +71,12 @@ def lib():
                                  ctypes.c_uint32]
         L.so_candidates.restype = ctypes.c_int64
         L.so_candidates.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P]
+        L.so_batch_create.restype = P
+        L.so_batch_create.argtypes = [ctypes.POINTER(SoCfg), ctypes.c_int64, ctypes.c_uint32]
+        L.so_batch_destroy.argtypes = [P]
+        L.so_batch_reset.argtypes = [P, P, ctypes.c_int]
+        L.so_batch_step.argtypes = [P, P, P, P, P, P, P, P, P, ctypes.c_int]
+        L.so_batch_grids.argtypes = [P, P]
         _lib = L
     return _lib
 
@@ -169,6 +175,59 @@ class OracleEnv:
                              int(alive_snakes), int(episode_length))
         if rc != 0:
             raise ValueError('inject failed')
+
+
+class OracleBatch:
+    """n oracle envs (env i == SnakeEnv after np.random.seed(seed + i)) stepped
+    together on `threads` host threads with the vector env's auto-reset; outputs
+    shaped like SnakeVecEnv.step's (so_batch_step)."""
+
+    def __init__(self, n, seed=0, threads=None, **cfg):
+        self.cfg = make_cfg(**cfg)
+        self.n, self.S = int(n), self.cfg.num_snakes
+        self.H, self.W = self.cfg.height, self.cfg.width
+        vr = self.cfg.vision_range
+        oh = ow = 2 * vr + 1 if vr else None
+        if not vr:
+            oh, ow = self.H, self.W
+        self.obs_shape = (self.n, self.S, oh, ow, 8 * self.cfg.frame_stack)
+        self.threads = int(threads or min(16, len(os.sched_getaffinity(0))))
+        self._h = lib().so_batch_create(ctypes.byref(self.cfg), self.n, ctypes.c_uint32(seed & 0xffffffff))
+        if not self._h:
+            raise ValueError('invalid oracle config')
+
+    def __del__(self):
+        h = getattr(self, '_h', None)
+        if h:
+            lib().so_batch_destroy(h)
+            self._h = None
+
+    def reset(self):
+        obs = np.zeros(self.obs_shape, np.uint8)
+        lib().so_batch_reset(self._h, _ptr(obs), self.threads)
+        return obs
+
+    def step(self, actions):
+        a = np.ascontiguousarray(np.asarray(actions).astype(np.int8).reshape(self.n, self.S))
+        n, S = self.n, self.S
+        obs = np.zeros(self.obs_shape, np.uint8)
+        rew = np.zeros((n, S), np.float64)
+        done = np.zeros((n, S), np.uint8)
+        ep_done = np.zeros(n, np.uint8)
+        rank = np.zeros((n, S), np.int32)
+        ep_stats = np.zeros((n, 4, S), np.float64)
+        err = np.zeros(n, np.int32)
+        lib().so_batch_step(self._h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(done), _ptr(ep_done), _ptr(rank),
+                            _ptr(ep_stats), _ptr(err), self.threads)
+        info = {'episode_done': ep_done.astype(bool), 'rank': rank, 'episode_scores': ep_stats[:, 0],
+                'episode_steps': ep_stats[:, 1], 'episode_fruits': ep_stats[:, 2],
+                'episode_kills': ep_stats[:, 3], 'error': err}
+        return obs, rew, done.astype(bool), info
+
+    def grids(self):
+        g = np.zeros((self.n, self.H, self.W), np.uint8)
+        lib().so_batch_grids(self._h, _ptr(g))
+        return g
 
 
 def rollout(n_env, seed, steps, act_seed=12345, **cfg):

@@ -19,8 +19,9 @@ for s in "$@"; do
     case $s in
         build) step build 300 python -c "import __graft_entry__ as g; g.build()" ;;
         smoke) step smoke 300 python __graft_entry__.py smoke ;;
-        tests) step tests 300 python -m pytest tests -x -q -m gpu ;;
-        testsv) step tests 300 python -m pytest tests -q -m gpu -rf ;;
+        tests) step tests 1100 python -u -m pytest tests -x -v -m gpu --timeout 400 --timeout-method thread ;;
+        testsv) step tests 1100 python -u -m pytest tests -v -m gpu -rf --timeout 400 --timeout-method thread ;;
+        testsk) step tests 1100 python -u -m pytest tests -x -v -m gpu -k "$TESTK" --timeout 400 --timeout-method thread ;;
         bench) step bench 600 python bench.py ;;
         benchq) step bench 300 python bench.py --steps 200 --warmup 50 --cpu-seconds 5 ;;
         benchthr) for t in ${THRS:--1 1 2 3}; do

@@ -519,3 +519,146 @@ def test_autoreset_every_step_matches_oracle(oracle, S, kw):
             assert (rd == done[i]).all(), (t, i)
             assert bool(ep_done[i]) == bool(rinfo), (t, i)
             assert (r.reset() == obs[i]).all(), (t, i)
+
+
+def test_single_snake_vector_surface(oracle):
+    """make_snake(num_envs > 1, num_snakes=1): the reference wraps each vector
+    worker in SingleAgent (wrappers.py:84-105, 204-212), so obs (N, h, w, C),
+    actions (N,), rewards (N,) float64, dones (N,) bool -- replayed against the
+    oracle env by env (env i seeded i, all-done auto-reset)."""
+    from marlenv import make_snake
+    N = 24
+    kw = dict(height=10, width=10, vision_range=4, num_fruits=4)
+    env, _, _, props = make_snake(num_envs=N, num_snakes=1, **kw)
+    assert props == {'action_info': {'action_n': 3}, 'num_envs': N, 'num_snakes': 1}
+    assert env.observation_space.shape == (N, 9, 9, 8)
+    assert env.single_observation_space.shape == (9, 9, 8)
+    assert env.action_space.shape == (N,)
+    refs, o0 = oracle_batch(oracle, N, 0, 1, **kw)
+    obs = env.reset()
+    assert tuple(obs.shape) == (N, 9, 9, 8)
+    np.testing.assert_array_equal(_np(obs), o0[:, 0])
+    rs = np.random.RandomState(6)
+    ended = 0
+    for t in range(120):
+        a = rs.randint(0, 3, size=N)
+        obs, rew, done, info = env.step(torch.from_numpy(a))
+        assert tuple(obs.shape) == (N, 9, 9, 8) and tuple(rew.shape) == (N,) and tuple(done.shape) == (N,)
+        assert rew.dtype == torch.float64 and done.dtype == torch.bool
+        assert tuple(info['rank'].shape) == (N,) and tuple(info['episode_scores'].shape) == (N,)
+        ended += int(info['episode_done'].sum())
+        for i, r in enumerate(refs):
+            ro, rr, rd, rinfo = r.step(a[i:i + 1])
+            assert rr.tobytes() == _np(rew)[i:i + 1].tobytes(), (t, i)
+            assert bool(rd[0]) == bool(_np(done)[i]), (t, i)
+            if rd[0]:
+                ro = r.reset()
+            np.testing.assert_array_equal(_np(obs)[i], ro[0], err_msg=f'step {t} env {i}')
+    assert ended > 0
+
+
+@pytest.mark.parametrize('kw,S', [(dict(height=20, width=20, vision_range=5), 4),
+                                  (dict(height=12, width=12, frame_stack=2), 2)])
+def test_every_step_invalid_action_keeps_obs(oracle, kw, S):
+    """autoreset='every_step' with an invalid action in some envs: those envs are
+    left unchanged (the reference raises KeyError before touching them) and their
+    returned obs is the observation of the unchanged state, not uninitialised
+    memory; every other env is stepped and reset."""
+    from marlenv import SnakeVecEnv
+    N = 40
+    v = SnakeVecEnv(N, num_snakes=S, seed=13, autoreset='every_step', **kw)
+    refs, o0 = oracle_batch(oracle, N, 13, S, **kw)
+    assert (_np(v.reset()) == o0).all()
+    last = o0.copy()
+    rs = np.random.RandomState(9)
+    for t in range(12):
+        a = rs.randint(0, 3, size=(N, S))
+        bad = rs.rand(N) < 0.3
+        a[bad, 0] = 7
+        obs, rew, done, info = v.step(torch.from_numpy(a))
+        obs, rew, err = _np(obs), _np(rew), _np(info['error'])
+        for i, r in enumerate(refs):
+            if bad[i]:
+                assert err[i] == 1 and not rew[i].any()
+                np.testing.assert_array_equal(obs[i], last[i], err_msg=f'step {t} env {i}')
+                continue
+            assert err[i] == 0
+            _, rr, _, _ = r.step(a[i])
+            assert rr.tobytes() == rew[i].tobytes()
+            last[i] = r.reset()
+            np.testing.assert_array_equal(obs[i], last[i], err_msg=f'step {t} env {i}')
+
+
+def test_full_size_cfg2_every_env(oracle):
+    """BASELINE config 2 at full size (4 096 envs, 20x20, 4 snakes, full-map
+    obs): EVERY env against the oracle batch (oracle/snake_oracle.c so_batch,
+    host threads) for 400 steps -- obs, rewards (bytes), dones, the episode
+    summary, and every grid every 25 steps."""
+    from marlenv import SnakeVecEnv
+    N, S, T = 4096, 4, 400
+    kw = dict(height=20, width=20, snake_length=3)
+    v = SnakeVecEnv(N, num_snakes=S, seed=0, **kw)
+    ref = oracle.OracleBatch(N, seed=0, num_snakes=S, **kw)
+    np.testing.assert_array_equal(_np(v.reset()), ref.reset())
+    g = torch.Generator(device='cuda').manual_seed(2024)
+    n_ep = 0
+    for t in range(T):
+        a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        obs, rew, done, info = v.step(a)
+        robs, rrew, rdone, rinfo = ref.step(a.cpu().numpy())
+        where = f'cfg2 step {t}'
+        assert _np(rew).tobytes() == rrew.tobytes(), where
+        np.testing.assert_array_equal(_np(done), rdone, err_msg=where)
+        ed = _np(info['episode_done'])
+        np.testing.assert_array_equal(ed, rinfo['episode_done'], err_msg=where)
+        np.testing.assert_array_equal(_np(info['rank']), rinfo['rank'], err_msg=where)
+        for k in ('episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills'):
+            assert _np(info[k]).tobytes() == rinfo[k].tobytes(), (where, k)
+        if not np.array_equal(_np(obs), robs):
+            bad = np.nonzero((_np(obs) != robs).reshape(N, -1).any(1))[0]
+            raise AssertionError(f'{where}: obs differ in envs {bad[:8].tolist()}')
+        if t % 25 == 0:
+            np.testing.assert_array_equal(_np(v.grids()), ref.grids(), err_msg=where)
+        n_ep += int(ed.sum())
+    assert n_ep > 0.005 * N * T / 60
+
+
+def test_full_size_cfg5_sampled(oracle):
+    """BASELINE config 5's per-GPU shard at full size (8 192 envs, 40x40, 8
+    snakes, vision_range 5, frame_stack 4): sampled envs against the oracle for
+    500 steps (several worker rounds, the 40x40 draw records, spawn-ahead under
+    load), plus whole-batch crop invariants."""
+    from marlenv import SnakeVecEnv
+    N, S, T = 8192, 8, 500
+    kw = dict(height=40, width=40, snake_length=3, vision_range=5, frame_stack=4)
+    v = SnakeVecEnv(N, num_snakes=S, seed=0, **kw)
+    obs = v.reset()
+    idx = np.unique(np.concatenate([np.arange(4), np.linspace(0, N - 1, 24).astype(int),
+                                    np.random.RandomState(1).randint(0, N, 12)]))
+    refs = {int(i): oracle.OracleEnv(seed=int(i), num_snakes=S, **kw) for i in idx}
+    sel = torch.from_numpy(idx).cuda()
+    o0 = obs[sel].cpu().numpy()
+    for row, i in enumerate(idx):
+        assert (refs[int(i)].reset() == o0[row]).all()
+    g = torch.Generator(device='cuda').manual_seed(55)
+    n_ep = 0
+    for t in range(T):
+        a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        obs, rew, done, info = v.step(a)
+        n_ep += int(info['episode_done'].sum())
+        sub = {k: x[sel].cpu().numpy() for k, x in info.items()}
+        compare_step([refs[int(i)] for i in idx], range(len(idx)), a[sel].cpu().numpy(),
+                     obs[sel].cpu().numpy(), rew[sel].cpu().numpy(), done[sel].cpu().numpy(), sub,
+                     where=f'cfg5 step {t}')
+        if t % 25:
+            continue
+        # newest frame (channels 24-31): one own-head cell at the crop centre of
+        # every alive snake, none for a dead one
+        tab = v.snake_table()
+        alive = tab[..., 5].bool()
+        heads = obs[..., 24 + 5].sum(dim=(2, 3))
+        assert torch.equal(obs[:, :, 5, 5, 24 + 5].bool() | ~alive, torch.ones_like(alive))
+        assert torch.equal(heads[alive], torch.ones_like(heads[alive]))
+        assert int(heads[~alive].sum()) == 0
+        assert not bool(info['error'].any())
+    assert n_ep > 0

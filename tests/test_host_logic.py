@@ -75,3 +75,36 @@ def test_autoreset_codes():
         autoreset_code('sometimes')
     cfg, _ = build_cfg(autoreset='every_step')
     assert cfg.autoreset == 2
+
+
+def test_dqn_rejects_mismatched_state_dict():
+    """The DQN kernels hard-code the reference's layer widths (train_dqn.py:104-151):
+    a state dict with other conv/fc widths or bias lengths must raise before any
+    weight is packed (no GPU needed to reach the check)."""
+    torch = pytest.importorskip('torch')
+    from marlenv import _native
+    try:
+        _native.lib()
+    except _native.NativeError:
+        pytest.skip('libsnake_amd.so not built')
+    from marlenv.dqn import DQNForward
+    H = W = 11
+    C, A = 8, 3
+
+    def sd(**over):
+        d = {'conv1.weight': (32, C, 3, 3), 'conv1.bias': (32,), 'conv2.weight': (64, 32, 3, 3),
+             'conv2.bias': (64,), 'conv3.weight': (64, 64, 3, 3), 'conv3.bias': (64,),
+             'fc1.weight': (256, 64 * H * W), 'fc1.bias': (256,), 'fc2.weight': (128, 256), 'fc2.bias': (128,),
+             'fc3.weight': (A, 128), 'fc3.bias': (A,)}
+        d.update(over)
+        return {k: torch.zeros(v) for k, v in d.items()}
+
+    for over in ({'conv2.weight': (48, 32, 3, 3)}, {'fc2.weight': (128, 128)}, {'conv3.bias': (63,)},
+                 {'fc1.weight': (256, 64 * H * W + 1)}, {'fc3.bias': (A + 1,)}):
+        for precision in ('bf16', 'fp32'):
+            with pytest.raises(ValueError):
+                DQNForward(sd(**over), H, W, C, A, device='cpu', precision=precision)
+    bad = sd()
+    del bad['fc2.bias']
+    with pytest.raises(ValueError):
+        DQNForward(bad, H, W, C, A, device='cpu')

@@ -1,0 +1,65 @@
+"""The N>1 bench path executed on hardware: two ranks of
+bench.main on the one GPU of the box (gloo process group: RCCL refuses two ranks
+on one device), launched as child processes through torch.distributed.run
+exactly as the driver launches N GPUs. Each rank steps its contiguous shard
+(env i seeded with its global index, actions drawn for the whole batch and
+sliced), and the concatenated shard results must equal one process stepping the
+whole batch: final grids, MT19937 keys and positions, env records, the last
+observation and every env's summed rewards, bit for bit."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd, tmp_path, name):
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    log = tmp_path / f'{name}.log'
+    with open(log, 'w') as fp:
+        rc = subprocess.run(cmd, cwd=ROOT, env=env, stdout=fp, stderr=subprocess.STDOUT, timeout=300).returncode
+    text = log.read_text()
+    assert rc == 0, f'{name} exited {rc}:\n{text[-3000:]}'
+    return [json.loads(x) for x in text.splitlines() if x.startswith('{"metric"')]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('config,per', [('cfg3', 768), ('cfg5', 96)])
+def test_two_ranks_equal_one_process(tmp_path, config, per):
+    if not os.path.exists(os.path.join(ROOT, 'marl-snake_amd', 'marlenv', 'libsnake_amd.so')):
+        pytest.fail('libsnake_amd.so not built')
+    common = ['--steps', '40', '--warmup', '10', '--no-cpu-baseline', '--timing-stride', '4',
+              '--global-actions', '--config', config]
+    two = tmp_path / 'two'
+    lines = _run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+                  '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), 'bench.py', '--gpus', '2',
+                  '--dist-backend', 'gloo', '--envs-per-gpu', str(per), '--dump-dir', str(two)] + common,
+                 tmp_path, 'two')
+    assert len(lines) == 1, 'rank 0 prints exactly one JSON line'
+    line = lines[0]
+    assert line['n_gpus'] == 2 and line['config']['num_envs'] == 2 * per and line['scaling'] == 'weak'
+    assert line['value'] > 0 and line['steps'] == 40
+    one = tmp_path / 'one'
+    lines1 = _run([sys.executable, 'bench.py', '--envs-per-gpu', str(2 * per), '--dump-dir', str(one)] + common,
+                  tmp_path, 'one')
+    assert len(lines1) == 1 and lines1[0]['n_gpus'] == 1
+    full = np.load(one / 'rank0.npz')
+    parts = [np.load(two / f'rank{r}.npz') for r in range(2)]
+    assert [(int(p['lo']), int(p['hi'])) for p in parts] == [(0, per), (per, 2 * per)]
+    for key in ('grids', 'mt', 'mt_pos', 'env', 'obs', 'rew_sum'):
+        cat = np.concatenate([p[key] for p in parts])
+        assert cat.tobytes() == full[key].tobytes(), key
+    if config == 'cfg3':   # the rollout went through episode ends (auto-resets on both ranks)
+        assert all(int(p['env'][:, 1].min()) < 50 for p in parts)
