@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 11
+#define SNAKE_ABI_VERSION 12
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -56,6 +56,13 @@ typedef struct {
                                    2 live snakes, every env under coop; the environment
                                    variable SNAKE_SPAWN_THR overrides), -1 = off, k >= 1 =
                                    envs with at most k live snakes. Never changes results. */
+    int32_t spawn_budget_us;    /* time slice of the spawn-ahead jobs per snake_step, in us
+                                   from the reset workers' start: an attempt still drawing at
+                                   the slice's end is paused (status 3, its draws kept in
+                                   st->spawn_draws) and continued by a later step, or finished
+                                   by the env's reset. 0 = automatic (about the time the step's
+                                   observation encode takes; SNAKE_SPAWN_BUDGET_US overrides),
+                                   -1 = unlimited. Never changes results. */
 } snake_cfg;
 
 /* Byte sizes of every caller-allocated buffer for num_envs envs (snake_plan). */
@@ -68,7 +75,8 @@ typedef struct {
     int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos
                                                          (> 624: the key's twist is pending, position
                                                          624 + j = word j of the next key),
-                                                         spawn-ahead status (0 none, 1 partial, 2 ready),
+                                                         spawn-ahead status (0 none, 1 partial, 2 ready,
+                                                         3 an attempt in progress),
                                                          spawn failure (1: the last reset gave up, below) */
     int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */
     int64_t stats;      /* snake_epi_stat [N][S]         running episode score/steps/fruits/kills */
@@ -77,7 +85,12 @@ typedef struct {
     int64_t jscratch;   /* uint32 [min(N,2560)][round4(n_cand)+64] reset link tables, 0 when the
                                                          u16 draw record fits LDS (2*n_cand <= 36 KB) */
     int64_t spawn;      /* uint32 [N][656]               spawn-ahead record: MT key, MT pos and the
-                                                         S spawn-pose indices of the env's next reset */
+                                                         S spawn-pose indices of the env's next reset
+                                                         (word 648: the next draw index of a paused
+                                                         attempt) */
+    int64_t spawn_draws;/* uint16 [N][round8(n_cand)]    draws of paused spawn-ahead attempts (j_i at
+                                                         index i); 0 when attempts are not sliced
+                                                         (spawn-ahead off, or global link tables) */
     int64_t resetq;     /* int32  [3][64][cap] + [209*32] sharded auto-reset and spawn-ahead queues
                                                          + the step's counters, one per 128-B line
                                                          (zero between steps) */
@@ -117,6 +130,7 @@ typedef struct {        /* device state buffers (layouts in snake_layout) */
     const int16_t *cand;
     uint32_t *jscratch; /* may be NULL when layout.jscratch == 0 */
     uint32_t *spawn;
+    uint16_t *spawn_draws; /* may be NULL when layout.spawn_draws == 0 (attempts then run whole) */
     int32_t  *resetq;   /* zero-initialised once by the caller */
 } snake_state;
 

@@ -277,6 +277,13 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
     o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     o->spawn = N * kSpawnStride * 4;
+    // paused spawn-ahead attempts keep their draws here (u16 per draw index):
+    // only where attempts can be sliced -- spawn-ahead on (all-done auto-reset)
+    // and the draw record in LDS -- and while it stays below 32 GiB
+    if (c->autoreset == 1 && c->spawn_ahead != -1 && o->jscratch == 0) {
+        const int64_t bytes = N * round_up(o->n_cand, 8) * 2;
+        o->spawn_draws = bytes <= ((int64_t)32 << 30) ? bytes : 0;
+    }
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
         // kQShards) with room for every env of its blocks, + the step's counters
         // (kQCount, each in its own line)
@@ -385,6 +392,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // off by default: measured 0.121 vs 0.109 ms at cfg3 (the hit rate falls)
     static const char *ev_cap = getenv("SNAKE_SPAWN_CAP");
     k->spawn_cap = ev_cap ? (atoi(ev_cap) != 0) : 0;
+    static const char *ev_redo = getenv("SNAKE_SPAWN_REDO");
+#ifndef SNAKE_SPAWN_REDO_DEFAULT
+#define SNAKE_SPAWN_REDO_DEFAULT 0
+#endif
+    k->spawn_redo = ev_redo ? (atoi(ev_redo) != 0) : SNAKE_SPAWN_REDO_DEFAULT;
     k->q_envs_per_block = kWave / (k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16));
     {
         const int64_t blocks = (N + k->q_envs_per_block - 1) / k->q_envs_per_block;
@@ -396,7 +408,69 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     if (c->spawn_ahead != 0) k->spawn_thr = c->spawn_ahead < 0 ? -1 : c->spawn_ahead;
     else k->spawn_thr = ev ? atoi(ev) : (k->coop ? k->S : 2);
     if (k->autoreset != 1) k->spawn_thr = -1;   // (every-step resets: nothing to draw ahead)
+    // spawn-ahead time slice (include/snake_env.h spawn_budget_us): automatic =
+    // the time the step's encodes take at ~4.5 TB/s (the workers start ~6 us
+    // before them), so that the workers end with the encodes
+    k->draws_stride = lay.spawn_draws ? (int)round_up(lay.n_cand, 8) : 0;
+    {
+        static const char *ev_bud = getenv("SNAKE_SPAWN_BUDGET_US");
+        int64_t us = c->spawn_budget_us;
+        if (us == 0) {
+            const int64_t enc = (int64_t)k->S * k->oh * k->ow * 8 * k->fs + (int64_t)k->fs * k->HW;
+            // (at least 30 us: shorter slices left more resets to finish paused
+            // attempts than they saved, measured at cfg2)
+            us = ev_bud ? atoll(ev_bud) : std::max<int64_t>(30, 4 + N * enc / 4500000);
+        }
+#ifndef SNAKE_SLICE
+#define SNAKE_SLICE 1   // (0: whole attempts, for A/B builds)
+#endif
+        k->spawn_budget = (SNAKE_SLICE && us > 0 && k->draws_stride > 0 && k->spawn_thr >= 0)
+                              ? (int)std::min<int64_t>(us * 100, 1 << 30) : 0;
+    }
     k->lds_obs_bytes = off;
+    {   // lean encode (snake_kernels.hip encode_lean): zero-bordered frames in LDS
+        static const char *ev_lean = getenv("SNAKE_LEAN");
+#ifndef SNAKE_LEAN_DEFAULT
+#define SNAKE_LEAN_DEFAULT 1
+#endif
+        const bool want = ev_lean ? atoi(ev_lean) != 0 : SNAKE_LEAN_DEFAULT;
+        k->lp = k->vr ? (int)round_up(k->vr, 4) : 0;
+        k->pw = k->vr ? (int)round_up(k->W + k->lp + k->vr, 4) : k->W;
+        const int ph = k->H + 2 * k->vr;
+        k->pframe = (int)round_up((int64_t)ph * k->pw, 16);
+        k->ups = k->oh * k->ow * k->fs;
+        k->rowl = k->ow * k->fs;
+        auto mag = [](uint64_t d) { return (uint32_t)(((1ull << 32) + d - 1) / d); };
+        k->mag_ups = mag(k->ups); k->mag_rowl = mag(k->rowl); k->mag_fs = mag(k->fs);
+        k->mag_wpr = mag(std::max(1, k->W / 4));
+        k->lds_lean_bytes = (int)round_up((int64_t)k->fs * k->pframe, 16) + 4 * k->fs * kMaxSnakes;
+        // the reciprocals must be exact for every unit index and grid word
+        // (k_encode_lean: grids with W % 4 == 0, at most 32 prefetched frame dwords per lane)
+        bool exact = (k->units % 2) == 0 && k->units < (1 << 22) && k->lds_lean_bytes <= 48 * 1024 &&
+                     k->W % 4 == 0 && (int64_t)k->fs * k->HW / 4 <= 8 * kWave;
+        for (int64_t u = 0; exact && u < k->units; u++) {
+            const int64_t q = ((uint64_t)u * k->mag_ups) >> 32, r0 = u - q * k->ups;
+            const int64_t i = ((uint64_t)r0 * k->mag_rowl) >> 32, r1 = r0 - i * k->rowl;
+            const int64_t j = ((uint64_t)r1 * k->mag_fs) >> 32;
+            exact = q == u / k->ups && i == r0 / k->rowl && j == r1 / k->fs;
+        }
+        if (k->W % 4 == 0)
+            for (int64_t x = 0; exact && x < (int64_t)k->HW / 4; x++)
+                exact = (int64_t)(((uint64_t)x * k->mag_wpr) >> 32) == x / (k->W / 4);
+        k->lean = want && exact ? 1 : 0;
+    }
+    // envs per encode wave (k_encode_multi: the next env's ring prefetched into
+    // registers, at most 8 16-byte chunks per lane); SNAKE_ENC_PER_WAVE overrides
+    {
+        static const char *ev_epw = getenv("SNAKE_ENC_PER_WAVE");
+#ifndef SNAKE_EPW_DEFAULT
+#define SNAKE_EPW_DEFAULT 2
+#endif
+        // (measured: 2 with the lean encode at cfg3/cfg2; one env per wave otherwise)
+        int epw = ev_epw ? atoi(ev_epw) : (k->lean ? SNAKE_EPW_DEFAULT : 1);
+        if (k->ring_bytes > 8 * 1024) epw = 1;
+        k->enc_per_wave = std::max(1, std::min(epw, 64));
+    }
     // the reset workers never use the encode staging buffer: the draw record
     // overlays it (the workers' LDS is what k_encode's waves share the CUs with)
     k->lds_link = k->lds_stage;
@@ -423,6 +497,10 @@ static int check_state(const KCfg &k, const snake_state *st, bool need_all)
     }
     if (!k.link_in_lds && !st->jscratch) {
         set_error("snake_state.jscratch is required for this config (n_cand=%d)", k.n_cand);
+        return SNAKE_E_ARG;
+    }
+    if (k.spawn_budget && !st->spawn_draws) {
+        set_error("snake_state.spawn_draws is required for this config (layout.spawn_draws > 0)");
         return SNAKE_E_ARG;
     }
     (void)need_all;

@@ -19,6 +19,7 @@ constexpr int kStageMax = 8192;     // bytes of staged observation per encode gr
 constexpr int kSpawnStride = 656;   // u32 words per spawn-ahead record: key, pos, poses
 constexpr int kSpawnPos = 624;      // record word: MT position after the recorded attempts
 constexpr int kSpawnSel = 625;      // record words [625, 625 + S): spawn-pose indices
+constexpr int kSpawnI = 648;        // record word: next draw index of a paused attempt (status INPROG)
 // Queue counters (zero between steps). Every counter sits in a line of its own
 // (kQSpread words apart): same-line device-scope atomics from thousands of
 // waves serialise at the memory side.
@@ -34,9 +35,9 @@ constexpr int kQCount = kQDone + 1;                   // counters
 constexpr int kQCounters = kQCount * kQSpread;        // words
 
 // env record words
-enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, ENV_FAIL = 5 };
+enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, ENV_FAIL = 5, ENV_VOID = 6 };
 // spawn-ahead status (env word ENV_SPAWN)
-enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2 };
+enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2, SPAWN_INPROG = 3 };
 
 // Everything a kernel needs, by value (a kernel argument).
 struct KCfg {
@@ -69,7 +70,18 @@ struct KCfg {
     int spawn_prio;             // wave priority of the spawn-ahead jobs (resets: 3)
     int encode_prio;            // wave priority of k_encode (beside the reset workers)
     int spawn_cap;              // 1: other spawn-ahead jobs only in the workers' first round
+    int spawn_redo;             // 1: after a fruit draw voided its record, an env is queued again only
+                                //    once at most one snake lives (ENV_VOID marks the void)
     int diag;                   // count spawn-ahead hits/jobs (while timing is enabled)
+    int spawn_budget;           // spawn-ahead time slice per step, s_memrealtime ticks (100 MHz); 0 = none
+    int draws_stride;           // u16 entries per env in st.spawn_draws (0: attempts are not sliced)
+    int enc_per_wave;           // envs per k_encode wave (1: k_encode, else k_encode_multi with prefetch)
+    // lean encode (encode_lean): the frames copied into a zero-bordered LDS image
+    // (lp columns / vr rows of padding, pw bytes per row, pframe bytes per frame)
+    // so the crop needs no bounds test; unit -> (snake, row, col, frame) by
+    // multiply-high reciprocals of ups = oh*ow*fs, rowl = ow*fs, fs, and of W/4
+    int lean, lp, pw, pframe, lds_lean_bytes, ups, rowl;
+    uint32_t mag_ups, mag_rowl, mag_fs, mag_wpr;
     double rf, rk, rl, rw, rt, max_steps;
 };
 

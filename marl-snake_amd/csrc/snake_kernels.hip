@@ -49,9 +49,14 @@ __device__ unsigned long long g_spawn_jobs;   // spawn-ahead attempts run
 // Diagnostic build only: s_memtime stamps of env 0's wave at phase boundaries.
 __device__ unsigned long long g_stamps[64];
 __device__ unsigned long long g_counts[8];
-__device__ unsigned long long g_obsprof[768];   // realtime (100 MHz) of auto-resets / encodes / spawn jobs
+__device__ unsigned long long g_obsprof[1408];  // realtime (100 MHz) of auto-resets / encodes / spawn jobs,
+                                                // then 5 words per auto-reset: 4 phase ends + spawn status
 #define OBSPROF(slot, lane)                                                          \
     do { if ((lane) == 0) g_obsprof[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RPROF(ps, p, lane)                                                           \
+    do { if ((ps) >= 0 && (lane) == 0) g_obsprof[768 + 5 * (ps) + (p)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RPROF_VAL(ps, p, v, lane)                                                    \
+    do { if ((ps) >= 0 && (lane) == 0) g_obsprof[768 + 5 * (ps) + (p)] = (v); } while (0)
 #define STAMP(e, lane, idx)                                                        \
     do {                                                                           \
         if ((e) == 0) {                                                            \
@@ -91,6 +96,8 @@ __device__ unsigned long long g_obsprof[768];   // realtime (100 MHz) of auto-re
 #define LSTAMP(idx) do {} while (0)
 #define RNOW() 0ull
 #define OBSPROF(slot, lane) do {} while (0)
+#define RPROF(ps, p, lane) do {} while (0)
+#define RPROF_VAL(ps, p, v, lane) do { (void)(v); } while (0)
 #endif
 
 enum { C_EMPTY = 0, C_WALL = 1, C_FRUIT = 2, C_HEAD = 3, C_BODY = 4, C_TAIL = 5 };
@@ -439,12 +446,17 @@ __device__ __forceinline__ bool draw_round(uint32_t tw0, uint32_t tw1, int base,
 }
 
 
+// i_start >= 0 resumes a paused attempt at draw index i_start (the MT state in
+// m is the one it was paused with). With a deadline (s_memrealtime ticks, 0 =
+// none) the draws pause between key blocks once it has passed -- never before
+// the first block, so every call makes progress -- and the next draw index is
+// returned (0: the draws are done).
 template <typename NP>
-__device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, int lane,
-                              int e = -1)
+__device__ int mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, int lane,
+                             int e = -1, int i_start = -1, unsigned long long deadline = 0)
 {
-    int i = n - 1;
-    if (i < 1) return;
+    int i = i_start >= 0 ? i_start : n - 1;
+    if (i < 1) return 0;
     COUNT_DECL;
     uint32_t mask = gen_mask((uint32_t)i);
     int lo = (int)(mask >> 1) + 1;
@@ -461,6 +473,10 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
     // invariant ends the wave instead of hanging the GPU
     for (int guard = 0; i >= 1 && guard < (1 << 20); guard++) {
         if (m.pos >= kMtN) {
+            if (deadline && guard > 0 && __builtin_amdgcn_s_memrealtime() > deadline) {
+                COUNT_FLUSH(e, lane);
+                return i;   // paused: m holds the untwisted key, m.pos >= 624
+            }
             mt_twist(m, lane);
 #pragma unroll
             for (int t = 0; t < 10; t++) tk[t] = temper(m.w[t]);
@@ -488,6 +504,7 @@ __device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu1
         }
     }
     COUNT_FLUSH(e, lane);
+    return 0;
 }
 
 // Final arr[k] of the Fisher-Yates pass for k < S from the LDS draw record
@@ -618,6 +635,104 @@ __device__ void place_fruits(const KCfg &c, uint8_t *g, WaveMT &m, int k, uint16
     wave_sync();
 }
 
+
+// Bulk output streams (observations, grid frames) are stored write-through
+// (sc1): each line leaves the XCD's L2 when written instead of at the
+// end-of-kernel release, whose write-back of the dirty L2 lines otherwise sits
+// between the step's kernels (MI355X_MICROARCH.md, row 'boundary': + dirty
+// bytes / ~6 TB/s). `base` is wave-uniform (the buffer descriptor lives in
+// SGPRs), `off` the lane's byte offset below `bytes`.
+#ifndef SNAKE_WT_GRID
+#define SNAKE_WT_GRID 0    // grid frames (k_logic's commit, reset grids): measured neutral
+#endif
+#ifndef SNAKE_WT_OBS
+#define SNAKE_WT_OBS 0     // observations (k_encode, resets)
+#endif
+template <bool WT>
+__device__ __forceinline__ void st16_wt(void *base, uint32_t bytes, uint32_t off, uint4 v)
+{
+    if constexpr (WT) {
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+        v4u32 x;
+        x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 16 /* sc1 */);
+    } else {
+        (void)bytes;
+        reinterpret_cast<uint4 *>(base)[off >> 4] = v;   // (16-byte aligned: off % 16 == 0)
+    }
+}
+template <bool WT>
+__device__ __forceinline__ void st8_wt(void *base, uint32_t bytes, uint32_t off, uint2 v)
+{
+    if constexpr (WT) {
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+        typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+        v2u32 x;
+        x.x = v.x; x.y = v.y;
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)off, 0, 16 /* sc1 */);
+    } else {
+        (void)bytes;
+        reinterpret_cast<uint2 *>(base)[off >> 3] = v;    // (off % 8 == 0)
+    }
+}
+
+// The reset's fruits (SnakeEnv.reset :147-148 -> random_empty_coords,
+// grid_util.py:126-133) on the freshly painted board: its empty cells are the
+// interior minus the S*L disjoint snake cells, so no grid scan is needed.
+// Draws: randint(0, E, size=k) = the first k raws r in stream order with
+// (r & mask) <= E - 1 (one ballot per 64 raws, not one mt_draw per fruit).
+// Cells: the v-th empty cell in np.where's row-major order has interior index
+// y = the least fixed point of y = v + #{snake cells with interior index <= y}
+// (iterated from v: a snake cell is never a least fixed point). `cell` = lane's
+// snake cell (lanes < S*L), `vbuf` = k u16 of LDS scratch.
+__device__ void place_fruits_fresh(const KCfg &c, uint8_t *g, WaveMT &m, int k, int cell, uint16_t *vbuf,
+                                   int lane)
+{
+    const int Wi = c.W - 2, SL = c.S * c.L;
+    const uint32_t E = (uint32_t)((c.H - 2) * Wi - SL), rng = E - 1, mask = gen_mask(rng);
+    int got = rng == 0 ? k : 0;                // randint(0, 1) draws nothing: every value is 0
+    if (rng == 0 && lane < k) vbuf[lane] = 0;
+    while (got < k) {
+        if (m.pos >= kMtN) mt_twist(m, lane);
+        const int t = m.pos >> 6, l0 = m.pos & 63;
+        const uint32_t v = temper(word_at(m, t)) & mask;
+        const unsigned long long acc = __ballot(lane >= l0 && (t << 6) + lane < kMtN && v <= rng);
+        const int rank = got + mbcnt64(acc);
+        if (((acc >> lane) & 1ull) && rank < k) vbuf[rank] = (uint16_t)v;
+        const int n = __popcll(acc);
+        if (got + n >= k) {                     // the stream resumes after the k-th accept
+            const int b = __ffsll((long long)__ballot(((acc >> lane) & 1ull) && rank == k - 1)) - 1;
+            m.pos = (t << 6) + b + 1;
+            got = k;
+        } else {
+            got += n;
+            m.pos = min((t + 1) << 6, kMtN);
+        }
+    }
+    wave_sync();
+    const int yi = lane < SL ? ((int)__umulhi((uint32_t)cell, c.mag_W) - 1) * Wi +
+                                   (cell - (int)__umulhi((uint32_t)cell, c.mag_W) * c.W - 1)
+                             : INT_MAX;
+    for (int d = 0; d < k; d++) {
+        const int v = __builtin_amdgcn_readfirstlane((int)vbuf[d]);
+        int y = v;
+        for (int it = 0; it <= SL; it++) {
+            const int y1 = v + __popcll(__ballot(yi <= y));
+            if (y1 == y) break;
+            y = y1;
+        }
+        const int r = y / Wi;
+        if (lane == 0) g[(r + 1) * c.W + (y - r * Wi) + 1] = C_FRUIT;
+    }
+    wave_sync();
+}
+
+#ifndef SNAKE_RESET_ROWS
+#define SNAKE_RESET_ROWS 0
+#endif
+#ifndef SNAKE_FRESH_FRUITS
+#define SNAKE_FRESH_FRUITS 1
+#endif
 // ------------------------------------------------------------------ encode
 // _encode (snake_env.py:474-519) + frame stack (:444-472): for snake k the 8
 // channels [wall, fruit, other head/body/tail, own head/body/tail]; with a vision
@@ -674,10 +789,10 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
             uint4 v;
             v.x = (uint32_t)a; v.y = (uint32_t)(a >> 32);
             v.z = (uint32_t)b; v.w = (uint32_t)(b >> 32);
-            *reinterpret_cast<uint4 *>(obs_env + 16 * (int64_t)p) = v;
+            st16_wt<SNAKE_WT_OBS>(obs_env, 8u * U, 16u * p, v);
         } else {
-            *reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p) = a;
-            if (has_b) *reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p + 8) = b;
+            st8_wt<SNAKE_WT_OBS>(obs_env, 8u * U, 16u * p, make_uint2((uint32_t)a, (uint32_t)(a >> 32)));
+            if (has_b) st8_wt<SNAKE_WT_OBS>(obs_env, 8u * U, 16u * p + 8u, make_uint2((uint32_t)b, (uint32_t)(b >> 32)));
         }
         f += c.adv_f;
         if (f >= fs) { f -= fs; j++; }
@@ -687,6 +802,89 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
         if (i >= c.oh) { i -= c.oh; k++; }
         k += c.adv_k;
     }
+}
+
+// Lean encode (k_encode): the observation straight from a zero-bordered copy
+// of the env's frames in LDS (pf: frame s's grid cell (r, c) at s*pframe +
+// (r + vr)*pw + c + lp, zero around it), so a crop window never needs a bounds
+// test; base[s*16 + k] = the LDS offset of snake k's window origin in frame s
+// (0 for the full map). Lane = one 16-byte output chunk = two consecutive
+// units (8 obs bytes each: one cell of one frame): per unit one LDS byte read
+// and its one-hot channel (_encode :481-492), no LDS staging of the output, no
+// divergent branch.
+__device__ void encode_lean(const KCfg &c, const uint8_t *pf, const int *base, int slot0, uint8_t *obs_env,
+                            int lane)
+{
+    const int pairs = c.units >> 1;
+    for (int p = lane; p < pairs; p += kWave) {
+        const uint32_t u = 2u * (uint32_t)p;
+        int kk = (int)__umulhi(u, c.mag_ups);
+        const int r0 = (int)u - kk * c.ups;
+        int ii = (int)__umulhi((uint32_t)r0, c.mag_rowl);
+        const int r1 = r0 - ii * c.rowl;
+        int jj = (int)__umulhi((uint32_t)r1, c.mag_fs);
+        int ff = r1 - jj * c.fs;
+        uint32_t w[4];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            int s = slot0 + ff;
+            s -= (s >= c.fs) ? c.fs : 0;
+            const int v = pf[s * c.pframe + base[s * kMaxSnakes + kk] + ii * c.pw + jj];
+            const int id = div10(v), code = v - 10 * id;
+            const int ch = (v < 3) ? v - 1 : ((id == kk) ? code + 2 : code - 1);
+            const uint32_t bit = (v != 0) ? (1u << (8 * (ch & 3))) : 0u;
+            w[2 * h] = ch < 4 ? bit : 0u;
+            w[2 * h + 1] = ch < 4 ? 0u : bit;
+            if (h == 0) {   // the next unit: frame, then column, row, snake digits carry
+                ff++;
+                const bool cf = ff == c.fs;
+                ff = cf ? 0 : ff;
+                jj += cf;
+                const bool cj = jj == c.ow;
+                jj = cj ? 0 : jj;
+                ii += cj;
+                const bool ci = ii == c.oh;
+                ii = ci ? 0 : ii;
+                kk += ci;
+            }
+        }
+        st16_wt<SNAKE_WT_OBS>(obs_env, 8u * c.units, 16u * p, make_uint4(w[0], w[1], w[2], w[3]));
+    }
+}
+
+// env e's frames into the zero-bordered LDS image of encode_lean (the border
+// was zeroed by the caller and is never written) and its window origins.
+__device__ void stage_lean(const KCfg &c, const snake_state &st, int64_t e, uint8_t *pf, int *base, int lane)
+{
+    const uint8_t *ring = st.grid + e * c.ring_bytes;
+    const int tp = c.vr;
+    if ((c.W & 3) == 0) {
+        const int wpr = c.W >> 2, nw = c.H * wpr;
+        const uint32_t *r32 = reinterpret_cast<const uint32_t *>(ring);
+        uint32_t *p32 = reinterpret_cast<uint32_t *>(pf);
+        for (int s = 0; s < c.fs; s++)
+            for (int x = lane; x < nw; x += kWave) {
+                const int r = (int)__umulhi((uint32_t)x, c.mag_wpr), c4 = x - r * wpr;
+                p32[(s * c.pframe + (r + tp) * c.pw + c.lp) / 4 + c4] = r32[s * (c.grid_stride >> 2) + x];
+            }
+    } else {
+        for (int s = 0; s < c.fs; s++)
+            for (int x = lane; x < c.HW; x += kWave) {
+                const int r = (int)__umulhi((uint32_t)x, c.mag_W), cc = x - r * c.W;
+                pf[s * c.pframe + (r + tp) * c.pw + c.lp + cc] = ring[s * c.grid_stride + x];
+            }
+    }
+    const int fsS = c.fs * c.S;
+    if (lane < fsS) {
+        const int x = lane / c.S, k = lane - x * c.S;
+        const int p = st.ctr[e * fsS + lane];
+        base[x * kMaxSnakes + k] = c.vr ? (p >> 8) * c.pw + (p & 255) + c.lp - c.vr : 0;
+    }
+}
+
+__device__ __forceinline__ void zero_lean(const KCfg &c, uint8_t *pf, int lane)
+{
+    for (int q = lane; q < (c.fs * c.pframe) >> 4; q += kWave) reinterpret_cast<uint4 *>(pf)[q] = make_uint4(0, 0, 0, 0);
 }
 
 // Row-wise encode: lane = one (snake, frame, window row); the row's cells are
@@ -728,10 +926,10 @@ __device__ void encode_rows(const KCfg &c, const uint8_t *frames, const int *org
         uint8_t *out = obs_env + (int64_t)k0 * P;
         if (wide) {
             for (int q = lane; q < bytes >> 4; q += kWave)
-                reinterpret_cast<uint4 *>(out)[q] = reinterpret_cast<const uint4 *>(stage)[q];
+                st16_wt<SNAKE_WT_OBS>(out, (uint32_t)bytes, 16u * q, reinterpret_cast<const uint4 *>(stage)[q]);
         } else {
             for (int q = lane; q < bytes >> 3; q += kWave)
-                reinterpret_cast<uint2 *>(out)[q] = reinterpret_cast<const uint2 *>(stage)[q];
+                st8_wt<SNAKE_WT_OBS>(out, (uint32_t)bytes, 8u * q, reinterpret_cast<const uint2 *>(stage)[q]);
         }
         wave_sync();
     }
@@ -763,9 +961,36 @@ __device__ __forceinline__ int dir_of_diff(int diff, int W)
 // permutation(n_cand)[:S] drawn from the wave's MT, lane (sk, si) = cell si of
 // pose sk (-1 past S*L), q = the pose indices; true when the poses are disjoint
 // (_clear_overlap :568-574).
+// Draws [lo, hi] of env e's paused attempt, LDS record -> st.spawn_draws.
+__device__ void save_draws(const KCfg &c, const snake_state &st, int e, const lu16 *jarr, int lo, int hi,
+                           int lane)
+{
+    uint16_t *g = st.spawn_draws + (int64_t)e * c.draws_stride;
+    for (int x = lo + lane; x <= hi; x += kWave) g[x] = jarr[x];
+}
+
+// Draws [lo, n) of env e's earlier slices, st.spawn_draws -> the LDS record:
+// 8-byte chunks from the first aligned index (past n only the record's dummy
+// slots are overwritten), single entries below it.
+__device__ void load_draws(const KCfg &c, const snake_state &st, int e, lu16 *jarr, int lo, int lane)
+{
+    const uint16_t *g = st.spawn_draws + (int64_t)e * c.draws_stride;
+    const int lo4 = min((lo + 3) & ~3, c.n_cand);
+    if (lane < lo4 - lo) jarr[lo + lane] = g[lo + lane];
+    const uint64_t *g8 = reinterpret_cast<const uint64_t *>(g);
+    typedef __attribute__((address_space(3))) uint64_t lu64;
+    lu64 *j8 = (lu64 *)jarr;
+    for (int x = (lo4 >> 2) + lane; x < (c.n_cand + 3) >> 2; x += kWave) j8[x] = g8[x];
+}
+
+// One permutation attempt; i_start >= 0 resumes a paused one (its earlier
+// draws in st.spawn_draws). With a deadline the draws may pause: paused_i = the
+// next draw index (> 0), the attempt's own draws are in the LDS record at
+// indices (paused_i, top] and q/cell are not set; the caller saves the state.
 template <int MS, bool JL>
 __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, uint8_t *lds, int slot,
-                              int e, int attempt, int (&q)[MS], int &cell, int lane)
+                              int e, int attempt, int (&q)[MS], int &cell, int lane, int i_start = -1,
+                              unsigned long long deadline = 0, int *paused_i = nullptr)
 {
     const int S = c.S, L = c.L, SL = S * L;
     const int sk = lane / L, si = lane - sk * L;
@@ -773,7 +998,12 @@ __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, 
     if constexpr (JL) {
         // the u16 draw record in LDS: every index 1..n-1 is written, nothing to clear
         lu16 *jarr = (lu16 *)(lds + c.lds_link);
-        mt_perm_draws(mt, c.n_cand, S, jarr, c.n_cand, jarr, lane, e);
+        const int pi = mt_perm_draws(mt, c.n_cand, S, jarr, c.n_cand, jarr, lane, e, i_start, deadline);
+        if (pi > 0) {
+            *paused_i = pi;
+            return false;
+        }
+        if (i_start >= 0 && i_start < c.n_cand - 1) load_draws(c, st, e, jarr, i_start + 1, lane);
         STAMP(e, lane, 2 + 3 * min(attempt, 3));
         wave_sync();
         perm_trace_j<MS>(S, c.n_cand, jarr, q, lane);
@@ -826,8 +1056,9 @@ __device__ __forceinline__ int load_reset_mt(const snake_state &st, int64_t e, W
 // record continues the retries where the record left them.
 template <int MS, bool JL>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
-                         WaveMT &mt, uint8_t *lds, int slot, int spst, int lane)
+                         WaveMT &mt, uint8_t *lds, int slot, int spst, int lane, int ps = -1)
 {
+    RPROF_VAL(ps, 4, spst, lane);
     uint8_t *frames = lds + c.lds_frames;
     int *org = reinterpret_cast<int *>(lds + c.lds_centers);
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
@@ -846,10 +1077,13 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         // likelier than ~1e-6 per reset)
         int q[MS];
         bool ok = false;
+        // a paused spawn-ahead attempt is finished first (from its draw index)
+        const int i0 = spst == SPAWN_INPROG ? (int)st.spawn[(int64_t)e * kSpawnStride + kSpawnI] : -1;
         for (int attempt = 0; attempt < (1 << 16) && !ok; attempt++)
-            ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, attempt, q, cell, lane);
+            ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, attempt, q, cell, lane, attempt == 0 ? i0 : -1);
         failed = !ok;
     }
+    RPROF(ps, 0, lane);
     // make_grid (grid_util.py:14-20), then paint (:138-144)
     for (int x = lane; x < c.HW; x += kWave) {
         const int r = (int)__umulhi((uint32_t)x, c.mag_W), cc = x - r * W;   // x / W
@@ -883,13 +1117,19 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     }
     wave_sync();
     STAMP(e, lane, 20);
-    place_fruits(c, work, mt, c.num_fruits, fbuf, lane);        // :147-148
+    RPROF(ps, 1, lane);
+#if SNAKE_FRESH_FRUITS
+    if (!failed) place_fruits_fresh(c, work, mt, c.num_fruits, cell, fbuf, lane);   // :147-148
+    else
+#endif
+    place_fruits(c, work, mt, c.num_fruits, fbuf, lane);         // (overlapping snakes: count the grid)
     STAMP(e, lane, 21);
+    RPROF(ps, 2, lane);
     uint8_t *gbase = st.grid + (int64_t)e * c.fs * c.grid_stride;
     const int n16 = c.grid_stride >> 4;
     for (int q = lane; q < n16; q += kWave) {
         const uint4 v = reinterpret_cast<const uint4 *>(work)[q];
-        for (int s = 0; s < c.fs; s++) reinterpret_cast<uint4 *>(gbase + s * c.grid_stride)[q] = v;
+        for (int s = 0; s < c.fs; s++) st16_wt<SNAKE_WT_GRID>(gbase, (uint32_t)c.ring_bytes, (uint32_t)(s * c.grid_stride + 16 * q), v);
         for (int s = 0; s < c.fs - 1; s++) reinterpret_cast<uint4 *>(frames + s * c.grid_stride)[q] = v;
     }
     if (lane == 0) {
@@ -898,14 +1138,23 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = er;
         if (spst != SPAWN_NONE) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = SPAWN_NONE;   // record used up
         st.env[(int64_t)e * kEnvRec + ENV_FAIL] = failed ? 1 : 0;
+        st.env[(int64_t)e * kEnvRec + ENV_VOID] = 0;
         if (failed && o.err) o.err[e] = 2;
     }
     if (lane < 2 * S) reinterpret_cast<uint64_t *>(st.stats)[(int64_t)e * 2 * S + lane] = 0ull;   // _reset_epi_stats
     mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
     wave_sync();
     STAMP(e, lane, 22);
-    // (the direct encode: one env's obs is on the reset's critical path, where the
-    // staged row-wise encode's two extra LDS passes cost more than they save)
+    RPROF(ps, 3, lane);
+    // One env's obs is on the reset's critical path: up to 4 KB (cfg3's 3 872 B)
+    // the direct encode, where the staged row-wise encode's two extra LDS passes
+    // cost more than they save; larger observations (full maps, frame stacks)
+    // through the staging buffer, which the draw record no longer needs.
+#if SNAKE_RESET_ROWS
+    if (c.enc_group > 0 && c.units * 8 > 4096) encode_rows(c, frames, org, 0, o.obs + (int64_t)e * c.units * 8,
+                                                           lds + c.lds_stage, lane);
+    else
+#endif
     encode(c, frames, org, 0, o.obs + (int64_t)e * c.units * 8, lane);
     STAMP(e, lane, 23);
 }
@@ -964,14 +1213,14 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
     // ---- every load this step needs, issued up front
-    int4 er = make_int4(0, 0, 0, 0);
-    int spst = SPAWN_NONE;
+    int4 er = make_int4(0, 0, 0, 0), er2 = make_int4(0, 0, 0, 0);
     if (env_ok) {
         er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
         // loaded whatever the threshold: a step run with spawn-ahead off must
         // still void a record its fruit draws make stale
-        spst = st.env[(int64_t)e * kEnvRec + ENV_SPAWN];
+        er2 = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec + 4);
     }
+    const int spst = er2.x, voided = er2.z;   // ENV_SPAWN, ENV_VOID
     int4 rec = make_int4(0, 0, 0, 0);
     int act = 0;
     // the snake's running episode statistics, one 16-byte record (snake_epi_stat)
@@ -1130,10 +1379,10 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // one attempt of its next reset (this step's k_autoreset workers). Claimed
     // as if every respawn drew (a queued env whose record stays ready is skipped
     // by its job); the status word written below is the exact one.
-    const bool spawn_q = c.spawn_thr >= 0 && env_ok && !bad && !ep_end && (need ? true : spst != SPAWN_READY) &&
-                         __popc(am) <= c.spawn_thr;
     // urgent (at most one live snake: the reset is likely next) and other jobs
     const bool urgent = __popc(am) <= 1;
+    const bool spawn_q = c.spawn_thr >= 0 && env_ok && !bad && !ep_end && (need ? true : spst != SPAWN_READY) &&
+                         __popc(am) <= c.spawn_thr && (!c.spawn_redo || urgent || !voided);
     const unsigned long long pm = __ballot(spawn_q && urgent && k == 0);
     const unsigned long long pn = __ballot(spawn_q && !urgent && k == 0);
     int pbase = 0, nbase = 0;
@@ -1354,7 +1603,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         if (g == gg) { mtpos_new = mt.pos; mt_slow = true; }
     }
     // a draw from the MT state voids the env's spawn-ahead record
-    const int spst1 = (mt_slow || mtpos_new != mtpos) ? SPAWN_NONE : spst;
+    const bool drew = mt_slow || mtpos_new != mtpos;
+    const int spst1 = drew ? SPAWN_NONE : spst;
+    const int voided1 = (drew && spst != SPAWN_NONE) ? 1 : voided;   // (a record was wasted this episode)
 
     LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
@@ -1387,6 +1638,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         if ((pn >> lane) & 1ull) st.resetq[(2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn)] = e;
     }
     if (env_ok && k == 0 && !bad && spst1 != spst) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spst1;
+    if (env_ok && k == 0 && !bad && voided1 != voided) st.env[(int64_t)e * kEnvRec + ENV_VOID] = voided1;
     LSTAMP(49);
     int rank = 1;
     for (int j = 0; j < S; j++) rank += (__shfl(s0, gb + j) > s0);
@@ -1407,7 +1659,8 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     LSTAMP(46);
     // commit the new frames into their ring slots; records; crop centres
     {
-        uint4 *dst = reinterpret_cast<uint4 *>(st.grid);
+        uint8_t *gblk = st.grid + (int64_t)e0 * c.ring_bytes;   // this block's envs' rings
+        const uint32_t gbytes = (uint32_t)(min(E, c.N - e0) * c.ring_bytes);
         const uint4 *s4 = reinterpret_cast<const uint4 *>(lds);
         for (int q0 = 0; q0 < E * n16; q0 += kWave) {
             const int q = q0 + lane, gg = min((int)__umulhi((uint32_t)q, c.mag_n16), E - 1);
@@ -1415,7 +1668,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
             const int ng = __shfl(ncur, gg * G);
             const int bg = __shfl((int)bad, gg * G);
             if (q < E * n16 && e0 + gg < c.N && !bg)
-                dst[((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)ng * stride) / 16 + off] = s4[q];
+                st16_wt<SNAKE_WT_GRID>(gblk, gbytes, (uint32_t)(gg * c.ring_bytes + ng * stride + 16 * off), s4[q]);
         }
     }
     // crop centre = the own HEAD cell: the new head while alive, (0,0) when dead
@@ -1462,14 +1715,32 @@ __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, 
     }
 }
 
+// With a deadline (the step's spawn-ahead time slice, JL boards only) an
+// attempt still drawing when it passes is paused: its draws so far go to
+// st.spawn_draws, the key and position to the record, the next draw index to
+// record word kSpawnI, status INPROG; a later job (or the env's reset)
+// continues it from there.
 template <int MS, bool JL>
-__device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot, int lane)
+__device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot,
+                         unsigned long long deadline, int lane)
 {
     WaveMT mt;
     const int spst = load_reset_mt(st, e, mt, lane);
     if (spst == SPAWN_READY) return;
-    int q[MS], cell;
-    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, 0, q, cell, lane);
+    uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
+    const int i0 = spst == SPAWN_INPROG ? (int)rec[kSpawnI] : -1;
+    int q[MS], cell, pi = 0;
+    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, 0, q, cell, lane, i0, JL ? deadline : 0, &pi);
+    if (JL && pi > 0) {
+        save_draws(c, st, e, (const lu16 *)(lds + c.lds_link), pi + 1, i0 >= 0 ? i0 : c.n_cand - 1, lane);
+        mt_store(mt, rec, lane);
+        if (lane == 0) {
+            rec[kSpawnPos] = (uint32_t)mt.pos;
+            rec[kSpawnI] = (uint32_t)pi;
+            st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = SPAWN_INPROG;
+        }
+        return;
+    }
     store_spawn_record<MS>(c, st, e, mt, ok, q, lane);
 }
 
@@ -1522,6 +1793,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
+    // the spawn-ahead time slice of this step (KCfg.spawn_budget): no spawn job
+    // starts after it, and attempts still drawing pause at it
+    const unsigned long long deadline =
+        c.spawn_budget ? __builtin_amdgcn_s_memrealtime() + (unsigned long long)c.spawn_budget : 0ull;
     // the shard counts of the three queues, prefix-summed: queue index j lives
     // in the shard whose [excl, incl) holds it
     int *qc = st.resetq + kNumQ * kQShards * c.q_cap;
@@ -1566,8 +1841,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
                 const int spst = load_reset_mt(st, e, mt, lane);
                 if (c.diag && lane == 0 && spst == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
                 if (idx < 128) OBSPROF(idx, lane);
-                if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
-                else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
+                const int ps = idx < 128 ? idx : -1;
+                if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
+                else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
                 if (idx < 128) OBSPROF(128 + idx, lane);
             }
         } else if (idx < R + P) {
@@ -1576,11 +1852,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             else __builtin_amdgcn_s_setprio(2);
             const int j = idx - R;
             const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
-            if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
-            if (j < 128) OBSPROF(512 + j, lane);
-            if (c.link_in_lds) do_spawn<MS, true>(c, st, e, lds, blockIdx.x, lane);
-            else do_spawn<MS, false>(c, st, e, lds, blockIdx.x, lane);
-            if (j < 128) OBSPROF(640 + j, lane);
+            if (!deadline || __builtin_amdgcn_s_memrealtime() < deadline) {   // (else: queued again next step)
+                if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
+                if (j < 128) OBSPROF(512 + j, lane);
+                if (c.link_in_lds) do_spawn<MS, true>(c, st, e, lds, blockIdx.x, deadline, lane);
+                else do_spawn<MS, false>(c, st, e, lds, blockIdx.x, 0ull, lane);
+                if (j < 128) OBSPROF(640 + j, lane);
+            }
         }
         int v = 0;
         if (lane == 0) v = atomicAdd(&qc[(kQClaim + x) * kQSpread], 1);
@@ -1615,8 +1893,135 @@ __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state s
     if (c.encode_prio == 1) __builtin_amdgcn_s_setprio(1);      // (setprio takes an immediate)
     else if (c.encode_prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (c.encode_prio == 3) __builtin_amdgcn_s_setprio(3);
+#ifdef SNAKE_ENC_NULL
+    // diagnostic build: the obs bytes stored, nothing read or computed
+    for (int q = lane; q < (c.units * 8) >> 4; q += kWave)
+        reinterpret_cast<uint4 *>(o.obs + (int64_t)e * c.units * 8)[q] = make_uint4(0, 0, 0, 0);
+    return;
+#endif
     encode_env(c, st, o, e, lds, lane);
     if (prof_) OBSPROF(384 + (e >> 9), lane);
+}
+
+// k_encode over c.enc_per_wave consecutive envs per wave: the next env's grid
+// ring, current slot, crop centres and reset flag are loaded into registers
+// before this env's encode, so their memory round trip overlaps it (a
+// one-env wave waits for its ring with nothing else to do; the encode is
+// latency- and occupancy-bound beside the reset workers). NPF = 16-byte ring
+// chunks per lane kept in flight (ring_bytes <= NPF * 1024).
+template <int NPF>
+__global__ void __launch_bounds__(64) k_encode_multi(const KCfg c, const snake_state st, const snake_out o)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    if (c.encode_prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (c.encode_prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (c.encode_prio == 3) __builtin_amdgcn_s_setprio(3);
+    const int fs = c.fs, S = c.S, n16 = c.ring_bytes >> 4, fsS = fs * S;
+    uint8_t *frames = lds + c.lds_frames;
+    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
+    const int e_begin = blockIdx.x * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
+    // (one vector value, not an array: an array of uint4 carried across the
+    // loop was demoted to scratch)
+    typedef uint32_t pf_t __attribute__((ext_vector_type(4 * NPF)));
+    pf_t pf = {};
+    int pcur = 0, pctr = 0, pskip = 0;
+#define SNAKE_ENC_FETCH(EE)                                                                        \
+    do {                                                                                           \
+        const int64_t e_ = (EE);                                                                   \
+        const uint4 *src_ = reinterpret_cast<const uint4 *>(st.grid + e_ * c.ring_bytes);          \
+        _Pragma("unroll") for (int u = 0; u < NPF; u++) {   /* (clamped: no per-chunk branch) */   \
+            const uint4 x_ = src_[min(lane + u * kWave, n16 - 1)];                                 \
+            pf[4 * u] = x_.x; pf[4 * u + 1] = x_.y; pf[4 * u + 2] = x_.z; pf[4 * u + 3] = x_.w;     \
+        }                                                                                          \
+        pcur = st.env[e_ * kEnvRec + ENV_CUR];                                                     \
+        pctr = lane < fsS ? st.ctr[e_ * fsS + lane] : 0;                                           \
+        pskip = c.autoreset ? o.ep_done[e_] : 0;                                                   \
+    } while (0)
+    if (e_begin < e_end) SNAKE_ENC_FETCH(e_begin);
+    for (int e = e_begin; e < e_end; e++) {
+        const int cur = pcur, skip = pskip;   // (its reset writes the obs of a reset env)
+        if (!skip) {
+            uint4 *d4 = reinterpret_cast<uint4 *>(frames);
+#pragma unroll
+            for (int u = 0; u < NPF; u++)
+                d4[min(lane + u * kWave, n16 - 1)] = make_uint4(pf[4 * u], pf[4 * u + 1], pf[4 * u + 2], pf[4 * u + 3]);
+            if (lane < fsS) {
+                const int x = lane / S, k = lane - x * S;
+                org[x * kMaxSnakes + k] = pack_origin(c, pctr >> 8, pctr & 255);
+            }
+        }
+        if (e + 1 < e_end) SNAKE_ENC_FETCH(e + 1);   // in flight during this env's encode
+        if (!skip) {
+            wave_sync();
+            encode_obs(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lds, lane);
+            wave_sync();   // the LDS frames are rewritten for the next env
+        }
+    }
+#undef SNAKE_ENC_FETCH
+}
+
+// Lean encode over c.enc_per_wave consecutive envs per wave (W % 4 == 0): the
+// next env's frames (NPW dwords per lane), current slot, crop centres and
+// reset flag are loaded into registers while this env is encoded, one memory
+// round trip per env in the shadow of the previous encode; the zero border of
+// the LDS image is written once per wave. The LDS destination of every
+// prefetched dword is the same for every env (computed once).
+template <int NPW>
+__global__ void __launch_bounds__(64) k_encode_lean(const KCfg c, const snake_state st, const snake_out o)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    if (c.encode_prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (c.encode_prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (c.encode_prio == 3) __builtin_amdgcn_s_setprio(3);
+    uint8_t *pf = lds;
+    int *base = reinterpret_cast<int *>(lds + c.fs * c.pframe);
+    uint32_t *p32 = reinterpret_cast<uint32_t *>(pf);
+    const int wpr = c.W >> 2, nw = c.H * wpr, nwt = c.fs * nw, gsw = c.grid_stride >> 2, fsS = c.fs * c.S;
+    // per prefetched dword: ring word index and LDS dword index (clamped: the
+    // lanes past the end repeat the last word, same source, same destination)
+    int src[NPW], dst[NPW];
+#pragma unroll
+    for (int u = 0; u < NPW; u++) {
+        const int x = min(lane + u * kWave, nwt - 1);
+        const int s = x / nw, xx = x - s * nw;
+        const int r = (int)__umulhi((uint32_t)xx, c.mag_wpr), c4 = xx - r * wpr;
+        src[u] = s * gsw + xx;
+        dst[u] = (s * c.pframe + (r + c.vr) * c.pw + c.lp) / 4 + c4;
+    }
+    zero_lean(c, pf, lane);
+    const int e_begin = blockIdx.x * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
+    uint32_t w[NPW];
+    int pcur = 0, pctr = 0, pskip = 0;
+#define SNAKE_LEAN_FETCH(EE)                                                                       \
+    do {                                                                                           \
+        const int64_t e_ = (EE);                                                                   \
+        const uint32_t *r32_ = reinterpret_cast<const uint32_t *>(st.grid + e_ * c.ring_bytes);    \
+        _Pragma("unroll") for (int u = 0; u < NPW; u++) w[u] = r32_[src[u]];                       \
+        pcur = st.env[e_ * kEnvRec + ENV_CUR];                                                     \
+        pctr = lane < fsS ? st.ctr[e_ * fsS + lane] : 0;                                           \
+        pskip = c.autoreset ? o.ep_done[e_] : 0;                                                   \
+    } while (0)
+    if (e_begin < e_end) SNAKE_LEAN_FETCH(e_begin);
+    for (int e = e_begin; e < e_end; e++) {
+        const int cur = pcur, skip = pskip;   // (a reset env's obs is written by its reset)
+        wave_sync();                          // (the previous encode has read the LDS image)
+        if (!skip) {
+#pragma unroll
+            for (int u = 0; u < NPW; u++) p32[dst[u]] = w[u];
+            if (lane < fsS) {
+                const int x = lane / c.S, k = lane - x * c.S;
+                base[x * kMaxSnakes + k] = c.vr ? (pctr >> 8) * c.pw + (pctr & 255) + c.lp - c.vr : 0;
+            }
+        }
+        if (e + 1 < e_end) SNAKE_LEAN_FETCH(e + 1);   // in flight during this env's encode
+        if (!skip) {
+            wave_sync();
+            encode_lean(c, pf, base, cur + 1 == c.fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lane);
+        }
+    }
+#undef SNAKE_LEAN_FETCH
 }
 
 template <int MS>
@@ -1655,6 +2060,7 @@ __global__ void k_seed(const KCfg c, const snake_state st, uint32_t base, long l
     }
     st.env[(int64_t)e * kEnvRec + ENV_MTPOS] = kMtN;
     st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = SPAWN_NONE;
+    st.env[(int64_t)e * kEnvRec + ENV_VOID] = 0;
 }
 
 // rgb_from_grid (grid_util.py:164-175) of every env's current grid: a palette
@@ -1924,7 +2330,18 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     };
     auto launch_encode = [&]() {
         TimedLaunch t3("k_encode", s_enc);
-        hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, s_enc, k, st, o);
+        const int epw2 = k.enc_per_wave;
+        const int lds_enc = k.lean ? k.lds_lean_bytes : k.lds_obs_bytes;
+        const dim3 ge((k.N + epw2 - 1) / epw2);
+        const int n16 = k.ring_bytes >> 4;
+        const int npw = (k.fs * k.HW / 4 + kWave - 1) / kWave;   // frame dwords per lane (lean)
+        if (k.lean && npw <= 2) hipLaunchKernelGGL(k_encode_lean<2>, ge, block, lds_enc, s_enc, k, st, o);
+        else if (k.lean && npw <= 8) hipLaunchKernelGGL(k_encode_lean<8>, ge, block, lds_enc, s_enc, k, st, o);
+        else if (k.lean) hipLaunchKernelGGL(k_encode_lean<32>, ge, block, lds_enc, s_enc, k, st, o);
+        else if (epw2 <= 1) hipLaunchKernelGGL(k_encode, g1, block, lds_enc, s_enc, k, st, o);
+        else if (n16 <= kWave) hipLaunchKernelGGL(k_encode_multi<1>, ge, block, lds_enc, s_enc, k, st, o);
+        else if (n16 <= 2 * kWave) hipLaunchKernelGGL(k_encode_multi<2>, ge, block, lds_enc, s_enc, k, st, o);
+        else hipLaunchKernelGGL(k_encode_multi<8>, ge, block, lds_enc, s_enc, k, st, o);
         t3.close();
         return check_launch("k_encode");
     };
@@ -2022,11 +2439,11 @@ extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, in
 #endif
 
 #ifdef SNAKE_STAMPS
-extern "C" int snake_debug_obsprof(unsigned long long *out /* 768 */)
+extern "C" int snake_debug_obsprof(unsigned long long *out /* 1408 */)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_obsprof), sizeof(unsigned long long) * 768) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_obsprof), sizeof(unsigned long long) * 1408) != hipSuccess)
         return -1;
-    unsigned long long z[768] = {0};
+    unsigned long long z[1408] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(snake::g_obsprof), z, sizeof z);
     return 0;
 }

@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 11
+SNAKE_ABI_VERSION = 12
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
@@ -26,12 +26,14 @@ class SnakeCfg(ctypes.Structure):
                 ('rew_fruit', ctypes.c_double), ('rew_kill', ctypes.c_double),
                 ('rew_lose', ctypes.c_double), ('rew_win', ctypes.c_double),
                 ('rew_time', ctypes.c_double), ('max_episode_steps', ctypes.c_double),
-                ('coop', ctypes.c_int32), ('autoreset', ctypes.c_int32), ('spawn_ahead', ctypes.c_int32)]
+                ('coop', ctypes.c_int32), ('autoreset', ctypes.c_int32), ('spawn_ahead', ctypes.c_int32),
+                ('spawn_budget_us', ctypes.c_int32)]
 
 
 class SnakeLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
-        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'spawn', 'resetq', 'obs', 'rew',
+        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'spawn', 'spawn_draws', 'resetq',
+        'obs', 'rew',
         'done',
         'ep_done', 'rank', 'ep_stats', 'err', 'n_cand')] + [
         ('obs_h', ctypes.c_int32), ('obs_w', ctypes.c_int32), ('obs_c', ctypes.c_int32),
@@ -40,7 +42,7 @@ class SnakeLayout(ctypes.Structure):
 
 class SnakeState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
-        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'spawn', 'resetq')]
+        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'spawn', 'spawn_draws', 'resetq')]
 
 
 class SnakeOut(ctypes.Structure):

@@ -31,6 +31,70 @@ def _torch():
     return torch
 
 
+def _raw_stream(index):
+    """hipStream_t of the current stream of device `index` (0 = the null stream)."""
+    import torch
+    return torch._C._cuda_getCurrentRawStream(index)
+
+
+def _current_device():
+    import torch
+    return torch._C._cuda_getDevice()
+
+
+_INFO_KEYS = ('episode_done', 'rank', 'episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills',
+              'error')
+
+
+class _StepInfo(dict):
+    """info of one SnakeVecEnv.step: a dict whose tensors are views of the step's
+    output slab, made when first read (most callers never read most of them)."""
+    __slots__ = ('_env', '_slab')
+
+    def __init__(self, env, slab):
+        dict.__init__(self, dict.fromkeys(_INFO_KEYS))
+        self._env, self._slab = env, slab
+
+    def _make(self, k):
+        env, slab = self._env, self._slab
+        if k == 'episode_done':
+            return env._view(slab, 'ep_done')
+        if k == 'rank':
+            return env._view(slab, 'rank')
+        if k == 'error':
+            return env._view(slab, 'err')
+        return env._view(slab, 'ep_stats')[:, ('episode_scores', 'episode_steps', 'episode_fruits',
+                                               'episode_kills').index(k)]
+
+    def __getitem__(self, k):
+        v = dict.__getitem__(self, k)
+        if v is None:
+            v = self._make(k)
+            dict.__setitem__(self, k, v)
+        return v
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+    def __iter__(self):              # (not dict's: dict(info) / {**info} then go through __getitem__)
+        return iter(list(dict.keys(self)))
+
+    def keys(self):
+        return dict.keys(self)
+
+    def values(self):
+        return [self[k] for k in self]
+
+    def items(self):
+        return [(k, self[k]) for k in self]
+
+    def copy(self):
+        return {k: self[k] for k in self}
+
+    def __repr__(self):
+        return repr(self.copy())
+
+
 class SnakeVecEnv:
     def __init__(self, num_envs, num_snakes=4, device=None, seed=0, env_offset=0,
                  autoreset=True, coop=False, strict=False, lib_path=None, **env_kwargs):
@@ -49,8 +113,9 @@ class SnakeVecEnv:
         lay = SnakeLayout()
         check(L.snake_plan(ctypes.byref(self.cfg), N, ctypes.byref(lay)))
         self.layout = lay
-        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
-        dev = self.device
+        dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self._dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+        self.device = dev = torch.device('cuda', self._dev_index)
         self.obs_shape = (S, lay.obs_h, lay.obs_w, lay.obs_c)
         self.grid_shape = (self.cfg.height, self.cfg.width)
         self.action_n = 5 if self.cfg.observer == 1 else 3
@@ -69,6 +134,9 @@ class SnakeVecEnv:
         self.mt = buf(lay.mt, torch.int32)
         self.jscratch = buf(lay.jscratch, torch.int32) if lay.jscratch else None
         self.spawn = buf(lay.spawn, torch.int32)
+        # draws of paused spawn-ahead attempts: written before they are read, no zero fill
+        self.spawn_draws = (torch.empty(int(lay.spawn_draws) // 2, dtype=torch.int16, device=dev)
+                            if lay.spawn_draws else None)
         self.resetq = buf(lay.resetq, torch.int32)
         cap = int(lay.n_cand) * self.cfg.snake_length
         host = np.zeros(cap, np.int16)
@@ -79,7 +147,8 @@ class SnakeVecEnv:
             self.grid.data_ptr(), self.snake.data_ptr(), self.body.data_ptr(), self.env_rec.data_ptr(),
             self.ctr.data_ptr(), self.stats.data_ptr(), self.mt.data_ptr(), self.cand.data_ptr(),
             self.jscratch.data_ptr() if self.jscratch is not None else None,
-            self.spawn.data_ptr(), self.resetq.data_ptr())
+            self.spawn.data_ptr(), self.spawn_draws.data_ptr() if self.spawn_draws is not None else None,
+            self.resetq.data_ptr())
         with torch.cuda.device(dev):
             check(L.snake_seed(ctypes.byref(self.cfg), ctypes.byref(self._state), N, self.seed_base,
                                self.env_offset, self._stream()))
@@ -90,29 +159,55 @@ class SnakeVecEnv:
         self.action_space = spaces.Box(0, self.action_n - 1, (N, S), np.int64)
         self._reset_done = False
         self._palette = None
+        self._plan_slab()
+        # the step's ctypes call with its constant arguments prebuilt
+        self._cfg_ref, self._state_ref = ctypes.byref(self.cfg), ctypes.byref(self._state)
+        self._step_fn = L.snake_step
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
-        torch = _torch()
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return ctypes.c_void_p(_raw_stream(self._dev_index))
 
-    def _new_out(self):
+    # Output slab of one call (include/snake_env.h snake_out): every output of a
+    # step is a view of ONE fresh device allocation -- still fresh per step
+    # (train_dqn.py:297 keeps references to returned observations), but one
+    # allocator call instead of seven. (name, dtype, per-env shape) in C-ABI order.
+    _OUTS = ('obs', 'rew', 'done', 'ep_done', 'rank', 'ep_stats', 'err')
+
+    def _plan_slab(self):
         torch = _torch()
         N, S = self.num_envs, self.num_snakes
-        d = self.device
-        out = dict(
-            obs=torch.empty((N,) + self.obs_shape, dtype=torch.uint8, device=d),
-            rew=torch.empty((N, S), dtype=torch.float64, device=d),
-            done=torch.empty((N, S), dtype=torch.bool, device=d),
-            ep_done=torch.empty((N,), dtype=torch.bool, device=d),
-            rank=torch.empty((N, S), dtype=torch.int32, device=d),
-            ep_stats=torch.empty((N, 4, S), dtype=torch.float64, device=d),
-            err=torch.empty((N,), dtype=torch.int32, device=d))
-        so = SnakeOut(*(out[k].data_ptr() for k in ('obs', 'rew', 'done', 'ep_done', 'rank', 'ep_stats', 'err')))
-        return out, so
+        spec = dict(obs=(torch.uint8, self.obs_shape), rew=(torch.float64, (S,)), done=(torch.bool, (S,)),
+                    ep_done=(torch.bool, ()), rank=(torch.int32, (S,)), ep_stats=(torch.float64, (4, S)),
+                    err=(torch.int32, ()))
+        off, plan = 0, {}
+        for k in self._OUTS:
+            dt, shp = spec[k]
+            n = N * int(np.prod(shp, dtype=np.int64)) * torch.empty((), dtype=dt).element_size()
+            plan[k] = (off, n, dt, (N,) + tuple(shp))
+            off += (n + 255) // 256 * 256
+        self._slab_plan, self._slab_bytes = plan, off
+        self._so = SnakeOut()
+
+    def _new_out(self):
+        """(slab, SnakeOut with the slab's pointers); views via _view."""
+        torch = _torch()
+        slab = torch.empty(self._slab_bytes, dtype=torch.uint8, device=self.device)
+        base, so, plan = slab.data_ptr(), self._so, self._slab_plan
+        so.obs, so.rew, so.done, so.ep_done, so.rank, so.ep_stats, so.err = (
+            base + plan[k][0] for k in self._OUTS)
+        return slab, so
+
+    def _view(self, slab, k):
+        off, n, dt, shape = self._slab_plan[k]
+        v = slab[off:off + n]
+        return (v if dt == _torch().uint8 else v.view(dt)).view(shape)
 
     def _actions(self, actions):
         torch = _torch()
+        if (isinstance(actions, torch.Tensor) and actions.dtype == torch.int8 and actions.device == self.device
+                and actions.is_contiguous() and actions.numel() == self.num_envs * self.num_snakes):
+            return actions                          # the common case: device int8, used as is
         a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions))
         a = a.to(self.device)
         if a.dtype != torch.int8:
@@ -129,7 +224,7 @@ class SnakeVecEnv:
         Returns the (N, S, h, w, 8*fs) uint8 observation tensor (rows of envs not in
         mask are left uninitialised)."""
         torch = _torch()
-        out, so = self._new_out()
+        slab, so = self._new_out()
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.uint8).reshape(self.num_envs).contiguous()
@@ -139,7 +234,7 @@ class SnakeVecEnv:
                                       ctypes.byref(so), self._stream()))
         self._keep = m
         self._reset_done = True
-        return out['obs']
+        return self._view(slab, 'obs')
 
     def step(self, actions):
         """SnakeEnv.step (snake_env.py:301-414) for every env.
@@ -155,25 +250,30 @@ class SnakeVecEnv:
         All outputs are freshly allocated every call."""
         if not self._reset_done:
             raise RuntimeError('call reset() before step()')
-        torch = _torch()
         a = self._actions(actions)
-        out, so = self._new_out()
-        with torch.cuda.device(self.device):
-            check(self._L.snake_step(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
-                                     ctypes.c_void_p(a.data_ptr()), ctypes.byref(so), self._stream()))
+        slab, so = self._new_out()
+        # (the library launches on the stream's own device whatever device is
+        # current, snake_kernels.hip DeviceGuard; only the legacy null stream
+        # takes the current device, so select ours for it)
+        stream = _raw_stream(self._dev_index)
+        if stream or _current_device() == self._dev_index:
+            rc = self._step_fn(self._cfg_ref, self._state_ref, self.num_envs, a.data_ptr(), ctypes.byref(so), stream)
+        else:
+            with _torch().cuda.device(self.device):
+                rc = self._step_fn(self._cfg_ref, self._state_ref, self.num_envs, a.data_ptr(), ctypes.byref(so),
+                                   stream)
+        if rc < 0:
+            check(rc, self._L)
         self._keep = a
-        info = {'episode_done': out['ep_done'], 'rank': out['rank'],
-                'episode_scores': out['ep_stats'][:, 0], 'episode_steps': out['ep_stats'][:, 1],
-                'episode_fruits': out['ep_stats'][:, 2], 'episode_kills': out['ep_stats'][:, 3],
-                'error': out['err']}
-        if self.strict and bool(out['err'].any()):
-            err = out['err']
+        info = _StepInfo(self, slab)
+        if self.strict and bool(info['error'].any()):
+            err = info['error']
             bad = (err == 1).nonzero().flatten().tolist()
             if bad:
                 raise KeyError(f'invalid action for an alive snake in envs {bad[:8]}')
             raise RuntimeError(f'auto-reset gave up placing disjoint snakes in envs '
                                f'{(err == 2).nonzero().flatten().tolist()[:8]}')
-        return out['obs'], out['rew'], out['done'], info
+        return self._view(slab, 'obs'), self._view(slab, 'rew'), self._view(slab, 'done'), info
 
     def render_rgb(self):
         """rgb_from_grid of every env's current grid (grid_util.py:164-175), on the
@@ -225,13 +325,19 @@ class SnakeVecEnv:
         dev = torch.device(device) if device is not None else self.device
         torch.cuda.current_stream(self.device).synchronize()
         sd = {k: getattr(self, k).detach().to(dev, copy=True) for k in self._STATE_BUFFERS}
+        # a paused spawn-ahead attempt keeps its draws in spawn_draws, which is not
+        # saved: the snapshot marks it as no record (spawn-ahead never changes
+        # results, the attempt is simply redone)
+        er = sd['env_rec'].view(self.num_envs, 8)
+        er[:, 4].masked_fill_(er[:, 4] == 3, 0)
         sd['meta'] = self._snapshot_meta()
         return sd
 
     def _snapshot_meta(self):
         lay = self.layout
         return dict(abi=int(self._L.snake_abi_version()), num_envs=self.num_envs,
-                    cfg=[getattr(self.cfg, f) for f, _ in self.cfg._fields_ if f != 'spawn_ahead'],
+                    cfg=[getattr(self.cfg, f) for f, _ in self.cfg._fields_
+                         if f not in ('spawn_ahead', 'spawn_budget_us')],
                     sizes=[int(getattr(lay, k)) for k in ('grid', 'snake', 'body', 'env', 'ctr', 'stats',
                                                           'mt', 'spawn')],
                     seed=self.seed_base, env_offset=self.env_offset, reset_done=self._reset_done)

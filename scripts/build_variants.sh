@@ -7,7 +7,7 @@ set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/marl-snake_amd/build/var
 mkdir -p "$OUT"
-FLAGS="-O3 -fPIC -std=c++17 -ffp-contract=off --offload-arch=gfx950"
+FLAGS="-O3 -fPIC -std=c++17 -ffp-contract=off --offload-arch=gfx950 -mllvm -amdgpu-atomic-optimizer-strategy=None"
 for spec in "$@"; do
     if [[ $spec == *@* ]]; then
         tag=${spec%@*}; rev=${spec#*@}

@@ -62,6 +62,21 @@ for s in "$@"; do
              step pmcF 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcF -o pmc -- $B
              step pmcW 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcW -o pmc -- $B
              step pmcSQ 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcSQ -o pmc -- $B ;;
+        hostov) step hostov 300 python scripts/host_overhead.py ;;
+        counters) step counters 60 rocprofv3 -L ;;
+        prof3) for c in ${CFGS:-cfg3}; do
+                   step prof_$c 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$c -o run --output-format csv -- python3 bench.py --config $c --steps 300 --warmup 100 --no-cpu-baseline --timing-stride 0
+               done ;;
+        pmcA) K='k_logic|k_autoreset|k_encode'
+              B="python3 bench.py --config ${CFG:-cfg3} --steps 40 --warmup 60 --no-cpu-baseline --timing-stride 0"
+              step pmcA 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcA -o pmc -- $B ;;
+        pmcB) K='k_logic|k_autoreset|k_encode'
+              B="python3 bench.py --config ${CFG:-cfg3} --steps 40 --warmup 60 --no-cpu-baseline --timing-stride 0"
+              step pmcB 300 rocprofv3 --pmc $PMCB --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcB -o pmc -- $B ;;
+        pmcTr) K='k_logic|k_autoreset|k_encode'
+               B="python3 bench.py --config ${CFG:-cfg3} --steps 40 --warmup 60 --no-cpu-baseline --timing-stride 0"
+               step pmcF 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcF -o pmc -- $B
+               step pmcW 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcW -o pmc -- $B ;;
         dqn) step dqn 300 python scripts/dqn_bench.py ;;
         dqnprof) step dqnprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dqnprof -o run --output-format csv -- python3 scripts/dqn_bench.py --no-torch ;;
         dqnpmc) step dqnpmc 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --kernel-include-regex k_dqn --output-format csv -d gpurun_out/dqnpmc -o pmc -- python3 scripts/dqn_bench.py --no-torch --steps 3 --warmup 1 ;;

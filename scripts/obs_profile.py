@@ -20,17 +20,27 @@ import torch  # noqa: E402
 from marlenv import SnakeVecEnv  # noqa: E402
 
 
+CFGS = {'cfg3': (65536, 4, dict(height=20, width=20, snake_length=3, vision_range=5)),
+        'cfg2': (4096, 4, dict(height=20, width=20, snake_length=3)),
+        'cfg5': (8192, 8, dict(height=40, width=40, snake_length=3, vision_range=5, frame_stack=4))}
+
+
 def main():
-    lib = os.path.abspath(sys.argv[1])
-    N = 65536
-    v = SnakeVecEnv(N, num_snakes=4, seed=0, lib_path=lib, height=20, width=20, snake_length=3, vision_range=5)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument('lib')
+    ap.add_argument('--cfg', default='cfg3', choices=sorted(CFGS))
+    a = ap.parse_args()
+    lib = os.path.abspath(a.lib)
+    N, S, kw = CFGS[a.cfg]
+    v = SnakeVecEnv(N, num_snakes=S, seed=0, lib_path=lib, **kw)
     L = ctypes.CDLL(lib)
     L.snake_debug_obsprof.argtypes = [ctypes.c_void_p]
     L.snake_debug_stamps.argtypes = [ctypes.c_void_p]
     st = np.zeros(72, dtype=np.uint64)
-    buf = np.zeros(768, dtype=np.uint64)
+    buf = np.zeros(1408, dtype=np.uint64)
     g = torch.Generator(device='cuda').manual_seed(7)
-    acts = torch.randint(0, 3, (300, N, 4), generator=g, device='cuda', dtype=torch.int8)
+    acts = torch.randint(0, 3, (300, N, S), generator=g, device='cuda', dtype=torch.int8)
     v.reset()
     for t in range(250):
         v.step(acts[t])
@@ -48,6 +58,7 @@ def main():
         b = buf.astype(np.int64)
         rs, re_, es, ee = b[:128], b[128:256], b[256:384], b[384:512]
         ss, se = b[512:640], b[640:768]
+        ph = b[768:768 + 5 * 128].reshape(128, 5)[:min(nres, 128)]
         sok = (ss > 0) & (se > 0)
         nr = min(nres, 128)
         rs, re_ = rs[:nr], re_[:nr]
@@ -66,6 +77,11 @@ def main():
             'spawn_start_us': pct(us(ss[sok])) if sok.any() else None,
             'spawn_end_us': pct(us(se[sok])) if sok.any() else None,
             'spawn_dur_us': pct((se[sok] - ss[sok]) / 100.0) if sok.any() else None,
+            # per reset: status at start (0 none, 1 partial, 2 ready, 3 in progress) and the
+            # phase durations: poses, paint, fruits, grid/key stores, encode
+            'reset_phases_us': [[int(p[4])] + [round(float(x), 1) for x in np.diff(
+                np.array([r, p[0], p[1], p[2], p[3], en], dtype=np.int64)) / 100.0]
+                for r, p, en in zip(rs, ph, re_)][:12],
         }), flush=True)
 
 

@@ -251,6 +251,10 @@ def test_full_size_sampled_parity(oracle):
 
 @pytest.mark.parametrize('S,kw,spawn', [
     (4, dict(height=20, width=20, vision_range=5), (0, -1, 1, 4)),
+    # sliced attempts (include/snake_env.h spawn_budget_us): 1-3 us slices pause
+    # nearly every attempt; later jobs and resets continue them
+    (4, dict(height=20, width=20, vision_range=5), ((0, -1), (0, 1), -1, (4, 2), 0)),
+    (8, dict(height=40, width=40, vision_range=5, frame_stack=2), ((0, -1), (0, 1), -1, (8, 3), 0)),
     (4, dict(height=12, width=12, coop=True), (0, -1)),             # coop: every env queued
     (8, dict(height=40, width=40, vision_range=5, frame_stack=2), (0, -1)),   # global link tables
 ])
@@ -260,7 +264,12 @@ def test_spawn_ahead_is_invisible(S, kw, spawn):
     resets from ready records."""
     from marlenv import SnakeVecEnv, _native
     N, T = 1024, 160
-    envs = [SnakeVecEnv(N, num_snakes=S, seed=77, spawn_ahead=sp, **kw) for sp in spawn]
+
+    def make(sp):
+        sp, bud = sp if isinstance(sp, tuple) else (sp, 0)
+        return SnakeVecEnv(N, num_snakes=S, seed=77, spawn_ahead=sp, spawn_budget_us=bud, **kw)
+    envs = [make(sp) for sp in spawn]
+    paused = 0
     outs = [v.reset() for v in envs]
     assert all(torch.equal(outs[0], o) for o in outs[1:])
     g = torch.Generator(device='cuda').manual_seed(4)
@@ -284,7 +293,10 @@ def test_spawn_ahead_is_invisible(S, kw, spawn):
             assert torch.equal(i0['episode_done'], i['episode_done'])
         for v in envs[1:]:
             assert torch.equal(envs[0].grids(), v.grids())
+        paused += sum(int((v.env_rec.view(N, 8)[:, 4] == 3).sum()) for v in envs)
     assert jobs > 0 and hits > 0
+    if any(isinstance(sp, tuple) for sp in spawn):
+        assert paused > 0, 'no attempt was ever paused'
 
 
 @pytest.mark.parametrize('S,kw', [(4, dict(height=20, width=20, vision_range=5)),
@@ -442,7 +454,8 @@ def test_info_zero_where_episode_continues():
 
 @pytest.mark.parametrize('kw,S', [(dict(height=20, width=20, vision_range=5), 4),
                                   (dict(height=12, width=12, frame_stack=3, vision_range=3, coop=True), 3),
-                                  (dict(height=44, width=44, vision_range=4, spawn_ahead=4), 4)])
+                                  (dict(height=44, width=44, vision_range=4, spawn_ahead=4), 4),
+                                  (dict(height=20, width=20, vision_range=5, spawn_budget_us=1), 4)])
 def test_snapshot_restore_roundtrip(kw, S):
     """state_dict() mid-episode -> K steps -> load_state_dict() -> the same K steps
     reproduce bit-identically, in the same env and in a fresh one (and from a
