@@ -215,9 +215,15 @@ def main():
         actions = torch.randint(0, 3, (n_act, hi - lo, S), generator=gen, device=device, dtype=torch.int8)
     rsum = torch.zeros((hi - lo, S), dtype=torch.float64, device=device) if args.dump_dir else None
 
+    # (outputs are dropped at once unless --dump-dir sums them: holding a step's
+    # outputs while the next step runs makes the allocator alternate between two
+    # observation buffers; measured +4 us per step at cfg3)
+    out = None
     for t in range(args.warmup):
-        out = venv.step(actions[t])
-        if rsum is not None:
+        if rsum is None:
+            venv.step(actions[t])
+        else:
+            out = venv.step(actions[t])
             rsum += out[1]
     torch.cuda.synchronize(device)
 
@@ -233,8 +239,10 @@ def main():
         timed = stride > 0 and t % stride == 0
         if timed:
             _native.timing_enable(True, L)
-        out = venv.step(actions[args.warmup + t])
-        if rsum is not None:
+        if rsum is None:
+            venv.step(actions[args.warmup + t])
+        else:
+            out = venv.step(actions[args.warmup + t])
             rsum += out[1]
         if timed:
             _native.timing_enable(False, L)

@@ -246,6 +246,22 @@ static double disjoint_prob(int H, int W, int L, int S, int64_t *samples)
 // probability happens for fewer than ~2e-6 of the resets.
 constexpr double kMinDisjoint = 2e-4;
 
+// The spawn-ahead time slice in us (include/snake_env.h spawn_budget_us), > 0
+// when attempts are sliced. Automatic (0): sliced only on boards whose attempt
+// outlasts a step's encodes (more than 8192 spawn poses, e.g. 40x40: ~115 us
+// per attempt under load; measured no gain at 20x20, cfg2/cfg3), the slice =
+// the time the step's encodes take at ~4.5 TB/s (the workers start ~6 us
+// before them), at least 30 us (shorter slices left more resets to finish
+// paused attempts than they saved); SNAKE_SPAWN_BUDGET_US overrides. (Without
+// N the sign is still right: it decides whether slicing is on.)
+static int64_t spawn_budget_us(const snake_cfg *c, int64_t n_cand, int64_t N = 0, int64_t enc_bytes = 0)
+{
+    static const char *ev_bud = getenv("SNAKE_SPAWN_BUDGET_US");
+    int64_t us = c->spawn_budget_us;
+    if (us == 0) us = ev_bud ? atoll(ev_bud) : (n_cand > 8192 ? std::max<int64_t>(30, 4 + N * enc_bytes / 4500000) : -1);
+    return us;
+}
+
 int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
 {
     int rc = check_cfg(c);
@@ -278,9 +294,9 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     o->spawn = N * kSpawnStride * 4;
     // paused spawn-ahead attempts keep their draws here (u16 per draw index):
-    // only where attempts can be sliced -- spawn-ahead on (all-done auto-reset)
-    // and the draw record in LDS -- and while it stays below 32 GiB
-    if (c->autoreset == 1 && c->spawn_ahead != -1 && o->jscratch == 0) {
+    // only where attempts are sliced (spawn_budget_us) -- spawn-ahead on
+    // (all-done auto-reset), the draw record in LDS -- and below 32 GiB
+    if (c->autoreset == 1 && c->spawn_ahead != -1 && o->jscratch == 0 && spawn_budget_us(c, o->n_cand) > 0) {
         const int64_t bytes = N * round_up(o->n_cand, 8) * 2;
         o->spawn_draws = bytes <= ((int64_t)32 << 30) ? bytes : 0;
     }
@@ -408,19 +424,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     if (c->spawn_ahead != 0) k->spawn_thr = c->spawn_ahead < 0 ? -1 : c->spawn_ahead;
     else k->spawn_thr = ev ? atoi(ev) : (k->coop ? k->S : 2);
     if (k->autoreset != 1) k->spawn_thr = -1;   // (every-step resets: nothing to draw ahead)
-    // spawn-ahead time slice (include/snake_env.h spawn_budget_us): automatic =
-    // the time the step's encodes take at ~4.5 TB/s (the workers start ~6 us
-    // before them), so that the workers end with the encodes
+    // spawn-ahead time slice (spawn_budget_us above)
     k->draws_stride = lay.spawn_draws ? (int)round_up(lay.n_cand, 8) : 0;
     {
-        static const char *ev_bud = getenv("SNAKE_SPAWN_BUDGET_US");
-        int64_t us = c->spawn_budget_us;
-        if (us == 0) {
-            const int64_t enc = (int64_t)k->S * k->oh * k->ow * 8 * k->fs + (int64_t)k->fs * k->HW;
-            // (at least 30 us: shorter slices left more resets to finish paused
-            // attempts than they saved, measured at cfg2)
-            us = ev_bud ? atoll(ev_bud) : std::max<int64_t>(30, 4 + N * enc / 4500000);
-        }
+        const int64_t enc = (int64_t)k->S * k->oh * k->ow * 8 * k->fs + (int64_t)k->fs * k->HW;
+        const int64_t us = spawn_budget_us(c, lay.n_cand, N, enc);
 #ifndef SNAKE_SLICE
 #define SNAKE_SLICE 1   // (0: whole attempts, for A/B builds)
 #endif

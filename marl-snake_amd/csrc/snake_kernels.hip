@@ -636,85 +636,24 @@ __device__ void place_fruits(const KCfg &c, uint8_t *g, WaveMT &m, int k, uint16
 }
 
 
-// Bulk output streams (observations, grid frames) are stored write-through
-// (sc1): each line leaves the XCD's L2 when written instead of at the
-// end-of-kernel release, whose write-back of the dirty L2 lines otherwise sits
-// between the step's kernels (MI355X_MICROARCH.md, row 'boundary': + dirty
-// bytes / ~6 TB/s). `base` is wave-uniform (the buffer descriptor lives in
-// SGPRs), `off` the lane's byte offset below `bytes`.
-#ifndef SNAKE_WT_GRID
-#define SNAKE_WT_GRID 0    // grid frames (k_logic's commit, reset grids): measured neutral
-#endif
-#ifndef SNAKE_WT_OBS
-#define SNAKE_WT_OBS 0     // observations (k_encode, resets)
-#endif
-template <bool WT>
-__device__ __forceinline__ void st16_wt(void *base, uint32_t bytes, uint32_t off, uint4 v)
-{
-    if constexpr (WT) {
-        const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
-        v4u32 x;
-        x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 16 /* sc1 */);
-    } else {
-        (void)bytes;
-        reinterpret_cast<uint4 *>(base)[off >> 4] = v;   // (16-byte aligned: off % 16 == 0)
-    }
-}
-template <bool WT>
-__device__ __forceinline__ void st8_wt(void *base, uint32_t bytes, uint32_t off, uint2 v)
-{
-    if constexpr (WT) {
-        const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
-        typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
-        v2u32 x;
-        x.x = v.x; x.y = v.y;
-        __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)off, 0, 16 /* sc1 */);
-    } else {
-        (void)bytes;
-        reinterpret_cast<uint2 *>(base)[off >> 3] = v;    // (off % 8 == 0)
-    }
-}
-
 // The reset's fruits (SnakeEnv.reset :147-148 -> random_empty_coords,
 // grid_util.py:126-133) on the freshly painted board: its empty cells are the
 // interior minus the S*L disjoint snake cells, so no grid scan is needed.
-// Draws: randint(0, E, size=k) = the first k raws r in stream order with
-// (r & mask) <= E - 1 (one ballot per 64 raws, not one mt_draw per fruit).
+// Draws: randint(0, E, size=k), one mt_draw each (all index the same empty
+// list: placing a fruit does not change E).
 // Cells: the v-th empty cell in np.where's row-major order has interior index
 // y = the least fixed point of y = v + #{snake cells with interior index <= y}
 // (iterated from v: a snake cell is never a least fixed point). `cell` = lane's
-// snake cell (lanes < S*L), `vbuf` = k u16 of LDS scratch.
-__device__ void place_fruits_fresh(const KCfg &c, uint8_t *g, WaveMT &m, int k, int cell, uint16_t *vbuf,
-                                   int lane)
+// snake cell (lanes < S*L).
+__device__ void place_fruits_fresh(const KCfg &c, uint8_t *g, WaveMT &m, int k, int cell, int lane)
 {
     const int Wi = c.W - 2, SL = c.S * c.L;
     const uint32_t E = (uint32_t)((c.H - 2) * Wi - SL), rng = E - 1, mask = gen_mask(rng);
-    int got = rng == 0 ? k : 0;                // randint(0, 1) draws nothing: every value is 0
-    if (rng == 0 && lane < k) vbuf[lane] = 0;
-    while (got < k) {
-        if (m.pos >= kMtN) mt_twist(m, lane);
-        const int t = m.pos >> 6, l0 = m.pos & 63;
-        const uint32_t v = temper(word_at(m, t)) & mask;
-        const unsigned long long acc = __ballot(lane >= l0 && (t << 6) + lane < kMtN && v <= rng);
-        const int rank = got + mbcnt64(acc);
-        if (((acc >> lane) & 1ull) && rank < k) vbuf[rank] = (uint16_t)v;
-        const int n = __popcll(acc);
-        if (got + n >= k) {                     // the stream resumes after the k-th accept
-            const int b = __ffsll((long long)__ballot(((acc >> lane) & 1ull) && rank == k - 1)) - 1;
-            m.pos = (t << 6) + b + 1;
-            got = k;
-        } else {
-            got += n;
-            m.pos = min((t + 1) << 6, kMtN);
-        }
-    }
-    wave_sync();
-    const int yi = lane < SL ? ((int)__umulhi((uint32_t)cell, c.mag_W) - 1) * Wi +
-                                   (cell - (int)__umulhi((uint32_t)cell, c.mag_W) * c.W - 1)
-                             : INT_MAX;
+    const int hr = (int)__umulhi((uint32_t)cell, c.mag_W);
+    const int yi = lane < SL ? (hr - 1) * Wi + (cell - hr * c.W - 1) : INT_MAX;
     for (int d = 0; d < k; d++) {
-        const int v = __builtin_amdgcn_readfirstlane((int)vbuf[d]);
+        // randint(0, E) (rng == 0: no raw consumed), the same mt_draw as the step's respawn
+        const int v = rng == 0 ? 0 : (int)mt_draw(m, mask, rng, lane);
         int y = v;
         for (int it = 0; it <= SL; it++) {
             const int y1 = v + __popcll(__ballot(yi <= y));
@@ -789,10 +728,10 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
             uint4 v;
             v.x = (uint32_t)a; v.y = (uint32_t)(a >> 32);
             v.z = (uint32_t)b; v.w = (uint32_t)(b >> 32);
-            st16_wt<SNAKE_WT_OBS>(obs_env, 8u * U, 16u * p, v);
+            *reinterpret_cast<uint4 *>(obs_env + 16 * (int64_t)p) = v;
         } else {
-            st8_wt<SNAKE_WT_OBS>(obs_env, 8u * U, 16u * p, make_uint2((uint32_t)a, (uint32_t)(a >> 32)));
-            if (has_b) st8_wt<SNAKE_WT_OBS>(obs_env, 8u * U, 16u * p + 8u, make_uint2((uint32_t)b, (uint32_t)(b >> 32)));
+            *reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p) = a;
+            if (has_b) *reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p + 8) = b;
         }
         f += c.adv_f;
         if (f >= fs) { f -= fs; j++; }
@@ -848,7 +787,7 @@ __device__ void encode_lean(const KCfg &c, const uint8_t *pf, const int *base, i
                 kk += ci;
             }
         }
-        st16_wt<SNAKE_WT_OBS>(obs_env, 8u * c.units, 16u * p, make_uint4(w[0], w[1], w[2], w[3]));
+        reinterpret_cast<uint4 *>(obs_env)[p] = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
 
@@ -926,10 +865,10 @@ __device__ void encode_rows(const KCfg &c, const uint8_t *frames, const int *org
         uint8_t *out = obs_env + (int64_t)k0 * P;
         if (wide) {
             for (int q = lane; q < bytes >> 4; q += kWave)
-                st16_wt<SNAKE_WT_OBS>(out, (uint32_t)bytes, 16u * q, reinterpret_cast<const uint4 *>(stage)[q]);
+                reinterpret_cast<uint4 *>(out)[q] = reinterpret_cast<const uint4 *>(stage)[q];
         } else {
             for (int q = lane; q < bytes >> 3; q += kWave)
-                st8_wt<SNAKE_WT_OBS>(out, (uint32_t)bytes, 8u * q, reinterpret_cast<const uint2 *>(stage)[q]);
+                reinterpret_cast<uint2 *>(out)[q] = reinterpret_cast<const uint2 *>(stage)[q];
         }
         wave_sync();
     }
@@ -1054,7 +993,7 @@ __device__ __forceinline__ int load_reset_mt(const snake_state &st, int64_t e, W
 // over the frame stack. `mt` comes from load_reset_mt: with a ready spawn-ahead
 // record the poses are the record's and the draws are already done; a partial
 // record continues the retries where the record left them.
-template <int MS, bool JL>
+template <int MS, bool JL, bool SLICE>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
                          WaveMT &mt, uint8_t *lds, int slot, int spst, int lane, int ps = -1)
 {
@@ -1078,7 +1017,8 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         int q[MS];
         bool ok = false;
         // a paused spawn-ahead attempt is finished first (from its draw index)
-        const int i0 = spst == SPAWN_INPROG ? (int)st.spawn[(int64_t)e * kSpawnStride + kSpawnI] : -1;
+        // (only sliced configurations pause attempts: SLICE)
+        const int i0 = SLICE && spst == SPAWN_INPROG ? (int)st.spawn[(int64_t)e * kSpawnStride + kSpawnI] : -1;
         for (int attempt = 0; attempt < (1 << 16) && !ok; attempt++)
             ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, attempt, q, cell, lane, attempt == 0 ? i0 : -1);
         failed = !ok;
@@ -1119,7 +1059,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     STAMP(e, lane, 20);
     RPROF(ps, 1, lane);
 #if SNAKE_FRESH_FRUITS
-    if (!failed) place_fruits_fresh(c, work, mt, c.num_fruits, cell, fbuf, lane);   // :147-148
+    if (!failed) place_fruits_fresh(c, work, mt, c.num_fruits, cell, lane);   // :147-148
     else
 #endif
     place_fruits(c, work, mt, c.num_fruits, fbuf, lane);         // (overlapping snakes: count the grid)
@@ -1129,7 +1069,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     const int n16 = c.grid_stride >> 4;
     for (int q = lane; q < n16; q += kWave) {
         const uint4 v = reinterpret_cast<const uint4 *>(work)[q];
-        for (int s = 0; s < c.fs; s++) st16_wt<SNAKE_WT_GRID>(gbase, (uint32_t)c.ring_bytes, (uint32_t)(s * c.grid_stride + 16 * q), v);
+        for (int s = 0; s < c.fs; s++) reinterpret_cast<uint4 *>(gbase + s * c.grid_stride)[q] = v;
         for (int s = 0; s < c.fs - 1; s++) reinterpret_cast<uint4 *>(frames + s * c.grid_stride)[q] = v;
     }
     if (lane == 0) {
@@ -1220,7 +1160,10 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         // still void a record its fruit draws make stale
         er2 = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec + 4);
     }
-    const int spst = er2.x, voided = er2.z;   // ENV_SPAWN, ENV_VOID
+#ifndef SNAKE_VOID
+#define SNAKE_VOID 1
+#endif
+    const int spst = er2.x, voided = SNAKE_VOID ? er2.z : 0;   // ENV_SPAWN, ENV_VOID
     int4 rec = make_int4(0, 0, 0, 0);
     int act = 0;
     // the snake's running episode statistics, one 16-byte record (snake_epi_stat)
@@ -1345,10 +1288,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     const uint32_t all_m = (1u << S) - 1u;
     const bool ep_end = !bad && (c.coop ? (done_m != 0u) : (done_m == all_m));
     if (c.coop && ep_end) fd = 1;
-    // (autoreset 2: every env, gym 0.23.1's reset after every step; an env
-    // rejected for an invalid action is queued too, for an encode of its
-    // unchanged state: no k_encode runs in that mode)
-    const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && (c.autoreset == 2 || (!bad && ep_end)))
+    // (autoreset 2: every env, gym 0.23.1's reset after every step, except an
+    // env rejected for an invalid action: k_encode encodes its unchanged state)
+    const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && !bad && (ep_end || c.autoreset == 2))
                                               : 0ull;
     const int shard = blockIdx.x % kQShards;
     int qbase = 0;
@@ -1638,7 +1580,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         if ((pn >> lane) & 1ull) st.resetq[(2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn)] = e;
     }
     if (env_ok && k == 0 && !bad && spst1 != spst) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spst1;
-    if (env_ok && k == 0 && !bad && voided1 != voided) st.env[(int64_t)e * kEnvRec + ENV_VOID] = voided1;
+    if (SNAKE_VOID && env_ok && k == 0 && !bad && voided1 != voided) st.env[(int64_t)e * kEnvRec + ENV_VOID] = voided1;
     LSTAMP(49);
     int rank = 1;
     for (int j = 0; j < S; j++) rank += (__shfl(s0, gb + j) > s0);
@@ -1659,8 +1601,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     LSTAMP(46);
     // commit the new frames into their ring slots; records; crop centres
     {
-        uint8_t *gblk = st.grid + (int64_t)e0 * c.ring_bytes;   // this block's envs' rings
-        const uint32_t gbytes = (uint32_t)(min(E, c.N - e0) * c.ring_bytes);
+        uint4 *dst = reinterpret_cast<uint4 *>(st.grid);
         const uint4 *s4 = reinterpret_cast<const uint4 *>(lds);
         for (int q0 = 0; q0 < E * n16; q0 += kWave) {
             const int q = q0 + lane, gg = min((int)__umulhi((uint32_t)q, c.mag_n16), E - 1);
@@ -1668,7 +1609,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
             const int ng = __shfl(ncur, gg * G);
             const int bg = __shfl((int)bad, gg * G);
             if (q < E * n16 && e0 + gg < c.N && !bg)
-                st16_wt<SNAKE_WT_GRID>(gblk, gbytes, (uint32_t)(gg * c.ring_bytes + ng * stride + 16 * off), s4[q]);
+                dst[((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)ng * stride) / 16 + off] = s4[q];
         }
     }
     // crop centre = the own HEAD cell: the new head while alive, (0,0) when dead
@@ -1720,7 +1661,7 @@ __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, 
 // st.spawn_draws, the key and position to the record, the next draw index to
 // record word kSpawnI, status INPROG; a later job (or the env's reset)
 // continues it from there.
-template <int MS, bool JL>
+template <int MS, bool JL, bool SLICE>
 __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot,
                          unsigned long long deadline, int lane)
 {
@@ -1730,8 +1671,9 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
     uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
     const int i0 = spst == SPAWN_INPROG ? (int)rec[kSpawnI] : -1;
     int q[MS], cell, pi = 0;
-    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, 0, q, cell, lane, i0, JL ? deadline : 0, &pi);
-    if (JL && pi > 0) {
+    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, 0, q, cell, lane, i0, SLICE ? deadline : 0ull,
+                                          &pi);
+    if (SLICE && pi > 0) {
         save_draws(c, st, e, (const lu16 *)(lds + c.lds_link), pi + 1, i0 >= 0 ? i0 : c.n_cand - 1, lane);
         mt_store(mt, rec, lane);
         if (lane == 0) {
@@ -1788,15 +1730,15 @@ __device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st,
     encode_obs(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lds, lane);
 }
 
-template <int MS>
+template <int MS, bool SLICE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KCfg c, const snake_state st, const snake_out o)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
-    // the spawn-ahead time slice of this step (KCfg.spawn_budget): no spawn job
-    // starts after it, and attempts still drawing pause at it
+    // the spawn-ahead time slice of this step (KCfg.spawn_budget, SLICE only): no
+    // spawn job starts after it, and attempts still drawing pause at it
     const unsigned long long deadline =
-        c.spawn_budget ? __builtin_amdgcn_s_memrealtime() + (unsigned long long)c.spawn_budget : 0ull;
+        SLICE ? __builtin_amdgcn_s_memrealtime() + (unsigned long long)c.spawn_budget : 0ull;
     // the shard counts of the three queues, prefix-summed: queue index j lives
     // in the shard whose [excl, incl) holds it
     int *qc = st.resetq + kNumQ * kQShards * c.q_cap;
@@ -1805,7 +1747,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     const int incl = wave_scan(cnt, lane), uincl = wave_scan(ucnt, lane), nincl = wave_scan(ncnt, lane);
     const int R = bcast(incl, kWave - 1), U = bcast(uincl, kWave - 1);
     // claim shards: min(G, kClaimShards), so that every shard has a worker
-    const int G = (int)gridDim.x, nsh = min(G, kClaimShards), x = blockIdx.x % nsh;
+    const int G = (int)gridDim.x, nsh = min(G, kClaimShards);
+    const int x = G >= kClaimShards ? (int)(blockIdx.x & (kClaimShards - 1)) : (int)blockIdx.x % nsh;
     // spawn_cap: the other (2-live-snake) jobs only as far as the first round
     // of workers reaches; their envs are queued again next step
     int Nn = bcast(nincl, kWave - 1);
@@ -1831,32 +1774,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
             const int e = job_env(0, idx, incl);
-            if (c.autoreset == 2 && o.err[e] == 1) {
-                // every-step mode, an env rejected for an invalid action: left
-                // unchanged (the reference raises before touching it), so its
-                // observation is the encode of its current frames
-                encode_env(c, st, o, e, lds, lane);
-            } else {
-                WaveMT mt;
-                const int spst = load_reset_mt(st, e, mt, lane);
-                if (c.diag && lane == 0 && spst == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
-                if (idx < 128) OBSPROF(idx, lane);
-                const int ps = idx < 128 ? idx : -1;
-                if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
-                else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
-                if (idx < 128) OBSPROF(128 + idx, lane);
-            }
+            WaveMT mt;
+            const int spst = load_reset_mt(st, e, mt, lane);
+            if (c.diag && lane == 0 && spst == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
+            if (idx < 128) OBSPROF(idx, lane);
+            const int ps = idx < 128 ? idx : -1;
+            if (c.link_in_lds) do_reset<MS, true, SLICE>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
+            else do_reset<MS, false, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
+            if (idx < 128) OBSPROF(128 + idx, lane);
         } else if (idx < R + P) {
             if (c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
             else if (c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(2);
             const int j = idx - R;
             const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
-            if (!deadline || __builtin_amdgcn_s_memrealtime() < deadline) {   // (else: queued again next step)
+            if (!SLICE || __builtin_amdgcn_s_memrealtime() < deadline) {   // (else: queued again next step)
                 if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
                 if (j < 128) OBSPROF(512 + j, lane);
-                if (c.link_in_lds) do_spawn<MS, true>(c, st, e, lds, blockIdx.x, deadline, lane);
-                else do_spawn<MS, false>(c, st, e, lds, blockIdx.x, 0ull, lane);
+                if (c.link_in_lds) do_spawn<MS, true, SLICE>(c, st, e, lds, blockIdx.x, deadline, lane);
+                else do_spawn<MS, false, false>(c, st, e, lds, blockIdx.x, 0ull, lane);
                 if (j < 128) OBSPROF(640 + j, lane);
             }
         }
@@ -1872,8 +1808,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     // step's counters for the next step: every worker has read its counts and
     // made its last claim by then (no host-side step parity, one extra atomic
     // per shard).
-    const int jobs_x = T > G + x ? (T - G - x + nsh - 1) / nsh : 0;
-    const int workers_x = (G - x + nsh - 1) / nsh;
+    const int jobs_x = T > G + x ? (nsh == kClaimShards ? (T - G - x + kClaimShards - 1) / kClaimShards
+                                                       : (T - G - x + nsh - 1) / nsh) : 0;
+    const int workers_x = nsh == kClaimShards ? (G - x + kClaimShards - 1) / kClaimShards : (G - x + nsh - 1) / nsh;
     if (nx == jobs_x + workers_x - 1) {
         int d = 0;
         if (lane == 0) d = atomicAdd(&qc[kQDone * kQSpread], 1);
@@ -1889,7 +1826,9 @@ __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state s
     const int e = blockIdx.x;
     const bool prof_ = (e & 511) == 0 && (e >> 9) < 128;
     if (prof_) OBSPROF(256 + (e >> 9), lane);
-    if (c.autoreset && o.ep_done[e]) return;          // its reset writes the obs
+    // a reset env's obs is written by its reset; in every-step mode only the
+    // envs rejected for an invalid action (left unchanged) are not reset
+    if (c.autoreset == 2 ? o.err[e] != 1 : (c.autoreset && o.ep_done[e])) return;
     if (c.encode_prio == 1) __builtin_amdgcn_s_setprio(1);      // (setprio takes an immediate)
     else if (c.encode_prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (c.encode_prio == 3) __builtin_amdgcn_s_setprio(3);
@@ -2037,8 +1976,8 @@ __global__ void __launch_bounds__(64) k_reset(const KCfg c, const snake_state st
         STAMP(e, lane, 0);
         WaveMT mt;
         const int spst = load_reset_mt(st, e, mt, lane);
-        if (c.link_in_lds) do_reset<MS, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
-        else do_reset<MS, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
+        if (c.link_in_lds) do_reset<MS, true, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
+        else do_reset<MS, false, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
         // with spawn-ahead on, the next reset's poses are drawn now, off the step
         if (c.spawn_thr >= 0) {
             if (c.link_in_lds) spawn_after_reset<MS, true>(c, st, e, mt, lds, blockIdx.x, lane);
@@ -2293,13 +2232,18 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;
-    if (k.autoreset == 2) {   // every env resets: no encode, the resets write every obs
+    if (k.autoreset == 2) {   // every env resets (the resets write the obs), then the
+                              // encodes of the envs rejected for an invalid action
         TimedLaunch t2("k_autoreset", sm);
-        if (k.S <= 4) hipLaunchKernelGGL(k_autoreset<4>, gr, block, k.lds_bytes, sm, k, st, o);
-        else if (k.S <= 8) hipLaunchKernelGGL(k_autoreset<8>, gr, block, k.lds_bytes, sm, k, st, o);
-        else hipLaunchKernelGGL(k_autoreset<16>, gr, block, k.lds_bytes, sm, k, st, o);
+        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false>), gr, block, k.lds_bytes, sm, k, st, o);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false>), gr, block, k.lds_bytes, sm, k, st, o);
+        else hipLaunchKernelGGL((k_autoreset<16, false>), gr, block, k.lds_bytes, sm, k, st, o);
         t2.close();
-        return check_launch("k_autoreset");
+        if ((rc = check_launch("k_autoreset"))) return rc;
+        TimedLaunch t3("k_encode", sm);
+        hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
+        t3.close();
+        return check_launch("k_encode");
     }
     if (!k.autoreset) {
         TimedLaunch t3("k_encode", sm);
@@ -2322,9 +2266,17 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     const hipStream_t s_res = resets_main ? sm : sc.side, s_enc = resets_main ? sc.side : sm;
     auto launch_resets = [&]() {
         TimedLaunch t2("k_autoreset", s_res);
-        if (k.S <= 4) hipLaunchKernelGGL(k_autoreset<4>, gr, block, k.lds_bytes, s_res, k, st, o);
-        else if (k.S <= 8) hipLaunchKernelGGL(k_autoreset<8>, gr, block, k.lds_bytes, s_res, k, st, o);
-        else hipLaunchKernelGGL(k_autoreset<16>, gr, block, k.lds_bytes, s_res, k, st, o);
+        // (the sliced form only where a time slice is set: its pause bookkeeping
+        // costs registers in every job)
+        if (k.spawn_budget) {
+            if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true>), gr, block, k.lds_bytes, s_res, k, st, o);
+            else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true>), gr, block, k.lds_bytes, s_res, k, st, o);
+            else hipLaunchKernelGGL((k_autoreset<16, true>), gr, block, k.lds_bytes, s_res, k, st, o);
+        } else {
+            if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false>), gr, block, k.lds_bytes, s_res, k, st, o);
+            else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false>), gr, block, k.lds_bytes, s_res, k, st, o);
+            else hipLaunchKernelGGL((k_autoreset<16, false>), gr, block, k.lds_bytes, s_res, k, st, o);
+        }
         t2.close();
         return check_launch("k_autoreset");
     };

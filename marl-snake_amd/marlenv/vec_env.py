@@ -168,10 +168,12 @@ class SnakeVecEnv:
     def _stream(self):
         return ctypes.c_void_p(_raw_stream(self._dev_index))
 
-    # Output slab of one call (include/snake_env.h snake_out): every output of a
-    # step is a view of ONE fresh device allocation -- still fresh per step
-    # (train_dqn.py:297 keeps references to returned observations), but one
-    # allocator call instead of seven. (name, dtype, per-env shape) in C-ABI order.
+    # Outputs of one call (include/snake_env.h snake_out): the observations in a
+    # fresh allocation of their own (a bare observation buffer that the caller
+    # drops is the one the next step gets back), every other output a view of
+    # ONE fresh slab -- fresh per step (train_dqn.py:297 keeps references to
+    # returned observations), two allocator calls instead of seven.
+    # (name, dtype, per-env shape) in C-ABI order.
     _OUTS = ('obs', 'rew', 'done', 'ep_done', 'rank', 'ep_stats', 'err')
 
     def _plan_slab(self):
@@ -184,23 +186,30 @@ class SnakeVecEnv:
         for k in self._OUTS:
             dt, shp = spec[k]
             n = N * int(np.prod(shp, dtype=np.int64)) * torch.empty((), dtype=dt).element_size()
+            if k == 'obs':
+                plan[k] = (0, n, dt, (N,) + tuple(shp))
+                continue
             plan[k] = (off, n, dt, (N,) + tuple(shp))
             off += (n + 255) // 256 * 256
         self._slab_plan, self._slab_bytes = plan, off
+        self._obs_shape_n = (N,) + tuple(self.obs_shape)
         self._so = SnakeOut()
 
     def _new_out(self):
-        """(slab, SnakeOut with the slab's pointers); views via _view."""
+        """((obs, slab), SnakeOut with their pointers); views via _view."""
         torch = _torch()
+        obs = torch.empty(self._obs_shape_n, dtype=torch.uint8, device=self.device)
         slab = torch.empty(self._slab_bytes, dtype=torch.uint8, device=self.device)
         base, so, plan = slab.data_ptr(), self._so, self._slab_plan
-        so.obs, so.rew, so.done, so.ep_done, so.rank, so.ep_stats, so.err = (
-            base + plan[k][0] for k in self._OUTS)
-        return slab, so
+        so.obs = obs.data_ptr()
+        so.rew, so.done, so.ep_done, so.rank, so.ep_stats, so.err = (base + plan[k][0] for k in self._OUTS[1:])
+        return (obs, slab), so
 
-    def _view(self, slab, k):
+    def _view(self, bufs, k):
+        if k == 'obs':
+            return bufs[0]
         off, n, dt, shape = self._slab_plan[k]
-        v = slab[off:off + n]
+        v = bufs[1][off:off + n]
         return (v if dt == _torch().uint8 else v.view(dt)).view(shape)
 
     def _actions(self, actions):
