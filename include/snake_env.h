@@ -60,9 +60,9 @@ typedef struct {
                                    from the reset workers' start: an attempt still drawing at
                                    the slice's end is paused (status 3, its draws kept in
                                    st->spawn_draws) and continued by a later step, or finished
-                                   by the env's reset. 0 = automatic (about the time the step's
-                                   observation encode takes; SNAKE_SPAWN_BUDGET_US overrides),
-                                   -1 = unlimited. Never changes results. */
+                                   by the env's reset. 0 = automatic (unlimited;
+                                   SNAKE_SPAWN_BUDGET_US overrides), -1 = unlimited. Never
+                                   changes results. */
 } snake_cfg;
 
 /* Byte sizes of every caller-allocated buffer for num_envs envs (snake_plan). */

@@ -247,18 +247,17 @@ static double disjoint_prob(int H, int W, int L, int S, int64_t *samples)
 constexpr double kMinDisjoint = 2e-4;
 
 // The spawn-ahead time slice in us (include/snake_env.h spawn_budget_us), > 0
-// when attempts are sliced. Automatic (0): sliced only on boards whose attempt
-// outlasts a step's encodes (more than 8192 spawn poses, e.g. 40x40: ~115 us
-// per attempt under load; measured no gain at 20x20, cfg2/cfg3), the slice =
-// the time the step's encodes take at ~4.5 TB/s (the workers start ~6 us
-// before them), at least 30 us (shorter slices left more resets to finish
-// paused attempts than they saved); SNAKE_SPAWN_BUDGET_US overrides. (Without
-// N the sign is still right: it decides whether slicing is on.)
+// when attempts are sliced. Automatic (0) = unlimited: slicing measured no gain
+// at 20x20 (cfg2/cfg3) and a loss at 40x40 (cfg5 step 0.1521 vs 0.1478 ms: the
+// paused attempts' resets and the sliced worker's register cost outweigh the
+// shorter tail); SNAKE_SPAWN_BUDGET_US overrides. N and enc_bytes are kept for
+// the A/B override's per-step scaling (0 < budget: as given).
 static int64_t spawn_budget_us(const snake_cfg *c, int64_t n_cand, int64_t N = 0, int64_t enc_bytes = 0)
 {
     static const char *ev_bud = getenv("SNAKE_SPAWN_BUDGET_US");
+    (void)n_cand; (void)N; (void)enc_bytes;
     int64_t us = c->spawn_budget_us;
-    if (us == 0) us = ev_bud ? atoll(ev_bud) : (n_cand > 8192 ? std::max<int64_t>(30, 4 + N * enc_bytes / 4500000) : -1);
+    if (us == 0) us = ev_bud ? atoll(ev_bud) : -1;
     return us;
 }
 

@@ -64,9 +64,9 @@ def test_plan_sizes(native):
     assert lay2.n_cand == 20168 and lay2.jscratch == 2560 * (20168 + 64) * 4   # global link tables
     assert lay.grid == 8192 * 4 * 1600
     # paused spawn-ahead attempts: u16 per draw index per env where attempts are
-    # sliced (automatic on boards of more than 8192 spawn poses, or an explicit
-    # spawn_budget_us; LDS draw record, spawn-ahead on), none otherwise
-    assert lay.spawn_draws == 8192 * 16424 * 2                    # 40x40: sliced by default
+    # sliced (an explicit spawn_budget_us; LDS draw record, spawn-ahead on),
+    # none otherwise
+    assert lay.spawn_draws == 0                                   # 40x40: not sliced by default
     assert lay2.spawn_draws == 0                                  # global link tables: not sliced
     for kw in (dict(autoreset=False), dict(autoreset='every_step'), dict(spawn_ahead=-1), {},
                dict(spawn_budget_us=-1)):

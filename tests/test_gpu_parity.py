@@ -254,7 +254,7 @@ def test_full_size_sampled_parity(oracle):
     # sliced attempts (include/snake_env.h spawn_budget_us): 1-3 us slices pause
     # nearly every attempt; later jobs and resets continue them
     (4, dict(height=20, width=20, vision_range=5), ((0, -1), (0, 5), -1, (4, 8))),
-    (8, dict(height=40, width=40, vision_range=5, frame_stack=2), ((0, -1), (0, 5), -1, (8, 12), 0)),
+    (8, dict(height=40, width=40, vision_range=5, frame_stack=2), ((0, -1), (0, 5), -1, (8, 12), (0, 30))),
     (4, dict(height=12, width=12, coop=True), (0, -1)),             # coop: every env queued
     (8, dict(height=40, width=40, vision_range=5, frame_stack=2), (0, -1)),   # global link tables
 ])
