@@ -228,7 +228,7 @@ def main():
     torch.cuda.synchronize(device)
 
     L = _native.lib()
-    for k in ('k_logic', 'k_autoreset', 'k_encode', 'resets', 'spawn_hits', 'spawn_jobs'):
+    for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_spawn', 'resets', 'spawn_hits', 'spawn_jobs'):
         _native.timing_read(k, L)                      # drop anything from the warmup
     stride = args.timing_stride
     if distributed:
@@ -252,7 +252,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kern = {}
-    for k in ('k_logic', 'k_autoreset', 'k_encode'):
+    for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_spawn'):
         ms, n = _native.timing_read(k, L)
         kern[k] = ms / max(n, 1)
     resets = _native.timing_read('resets', L)[1]

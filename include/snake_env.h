@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 12
+#define SNAKE_ABI_VERSION 13
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -63,6 +63,12 @@ typedef struct {
                                    by the env's reset. 0 = automatic (unlimited;
                                    SNAKE_SPAWN_BUDGET_US overrides), -1 = unlimited. Never
                                    changes results. */
+    int32_t spawn_background;   /* 1 = the spawn-ahead attempts run in a background kernel on a
+                                   stream of the library's that outlives snake_step (see
+                                   snake_sync), 0 = automatic (on for boards of more than 8192
+                                   spawn poses, e.g. 40x40; SNAKE_BG overrides), -1 = off (inside
+                                   the step). Needs spawn-ahead on, unsliced attempts and the
+                                   draw record in LDS. Never changes results. */
 } snake_cfg;
 
 /* Byte sizes of every caller-allocated buffer for num_envs envs (snake_plan). */
@@ -75,8 +81,9 @@ typedef struct {
     int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos
                                                          (> 624: the key's twist is pending, position
                                                          624 + j = word j of the next key),
-                                                         spawn-ahead status (0 none, 1 partial, 2 ready,
-                                                         3 an attempt in progress),
+                                                         spawn-ahead status (bits 0-1: 0 none, 1 partial,
+                                                         2 ready, 3 an attempt in progress; bits 2-31: the
+                                                         record's generation),
                                                          spawn failure (1: the last reset gave up, below) */
     int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */
     int64_t stats;      /* snake_epi_stat [N][S]         running episode score/steps/fruits/kills */
@@ -91,9 +98,9 @@ typedef struct {
     int64_t spawn_draws;/* uint16 [N][round8(n_cand)]    draws of paused spawn-ahead attempts (j_i at
                                                          index i); 0 when attempts are not sliced
                                                          (spawn-ahead off, or global link tables) */
-    int64_t resetq;     /* int32  [3][64][cap] + [209*32] sharded auto-reset and spawn-ahead queues
-                                                         + the step's counters, one per 128-B line
-                                                         (zero between steps) */
+    int64_t resetq;     /* int32  2 x ([3][64][cap] + [225*32]) sharded auto-reset and spawn-ahead
+                                                         queues + the step's counters, one per 128-B
+                                                         line; two sets, by step parity (zero-initialised) */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */
     int64_t rew;        /* double [N][S] */
     int64_t done;       /* uint8  [N][S] */
@@ -188,9 +195,17 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
  * identical with or without it (it only moves draws off the step's critical
  * path); cfg->spawn_ahead = -1 disables it. A caller that
  * rewrites an env's MT key or position itself must zero that env's status word
- * (env word 4). */
+ * (env word 4), after snake_sync. */
 int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
                const int8_t *actions, const snake_out *out, void *stream);
+
+/* With background spawn-ahead (cfg->spawn_background) a spawn kernel of the
+ * last snake_step may still be running when the call returns; it writes only
+ * st->spawn and env word 4, and the next snake_step / snake_reset / snake_seed
+ * order themselves after it. Before the caller reads or writes the state
+ * buffers itself (snapshots, set_mt_state, freeing them), snake_sync makes
+ * `stream` wait for it (a no-op without background work). */
+int snake_sync(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, void *stream);
 
 /* RGB image of every env's current grid: rgb_from_grid(grid, Cell, CellColors)
  * (grid_util.py:164-175), the frame of SnakeEnv.render('rgb_array') and of the

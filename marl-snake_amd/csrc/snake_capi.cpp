@@ -305,7 +305,7 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
         const int64_t E = kWave / (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
         const int64_t blocks = (N + E - 1) / E;
         const int64_t cap = (blocks + kQShards - 1) / kQShards * E;
-        o->resetq = (kNumQ * kQShards * cap + kQCounters) * 4;
+        o->resetq = kQSets * (kNumQ * kQShards * cap + kQCounters) * 4;
     }
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
@@ -433,6 +433,28 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
 #endif
         k->spawn_budget = (SNAKE_SLICE && us > 0 && k->draws_stride > 0 && k->spawn_thr >= 0)
                               ? (int)std::min<int64_t>(us * 100, 1 << 30) : 0;
+    }
+    // background spawn-ahead (snake_kernels.hip k_spawn): the jobs leave the
+    // step's critical window; with spawn-ahead on, all-done auto-reset, the draw
+    // record in LDS (the global link tables are per reset worker) and unsliced
+    // attempts. cfg->spawn_background: 0 automatic (SNAKE_BG overrides), 1 on, -1 off.
+    {
+        static const char *ev_bg = getenv("SNAKE_BG");
+#ifndef SNAKE_BG_DEFAULT
+#define SNAKE_BG_DEFAULT 1
+#endif
+        // automatic: boards of more than 8192 spawn poses, whose attempt outlasts a
+        // step (40x40: ~110 us; cfg5 step 0.149 -> 0.142 ms); at 20x20 the
+        // background jobs slowed the concurrent encodes more than they saved
+        // (cfg3 0.111 -> 0.124, cfg2 0.064 -> 0.065..0.078 ms)
+        const bool want = c->spawn_background != 0 ? c->spawn_background > 0
+                                                    : (ev_bg ? atoi(ev_bg) != 0
+                                                             : (SNAKE_BG_DEFAULT && lay.n_cand > 8192));
+        k->bg = (want && k->spawn_thr >= 0 && k->autoreset == 1 && k->spawn_budget == 0 &&
+                 2 * ((int64_t)lay.n_cand + kWave) <= kJarrLdsMax) ? 1 : 0;
+        static const char *ev_ss = getenv("SNAKE_SPAWN_SLOTS");
+        const int ss = ev_ss ? std::max(1, atoi(ev_ss)) : kResetSlots;
+        k->spawn_slots = (int)std::min<int64_t>(N, ss);
     }
     k->lds_obs_bytes = off;
     {   // lean encode (snake_kernels.hip encode_lean): zero-bordered frames in LDS
@@ -615,6 +637,15 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
     if ((rc = check_state(k, st, true))) return rc;
     if ((rc = check_out(out, false))) return rc;
     return launch_reset(k, *st, env_mask, *out, stream);
+}
+
+int snake_sync(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, void *stream)
+{
+    KCfg k;
+    int rc = plan_cached(cfg, num_envs, &k);
+    if (rc) return rc;
+    if (!st || !st->env) { set_error("snake_state.env is NULL"); return SNAKE_E_ARG; }
+    return wait_background(*st, stream);
 }
 
 int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, const int8_t *actions,

@@ -31,12 +31,19 @@ constexpr int kClaimShards = 16;    // claim counters: worker w claims on shard 
 constexpr int kNumQ = 3;            // queues: 0 resets, 1 urgent spawn-ahead (<= 1 live snake), 2 other spawn-ahead
 constexpr int kQClaim = kNumQ * kQShards;             // counter index of claim shard 0
 constexpr int kQDone = kQClaim + kClaimShards;        // counter index: claim shards drained
-constexpr int kQCount = kQDone + 1;                   // counters
+constexpr int kQSpClaim = kQDone + 1;                 // background spawn kernel (k_spawn): claim shard 0
+constexpr int kQCount = kQSpClaim + kClaimShards;     // counters
 constexpr int kQCounters = kQCount * kQSpread;        // words
+// The queues and counters exist twice (the step's parity, KCfg.qpar): with the
+// background spawn kernel a step's spawn-ahead queues are still being read while
+// the next step's k_logic fills the other set.
+constexpr int kQSets = 2;
+constexpr int kQGenBits = 6;        // spawn queue entry (background mode): env | generation << 26
 
 // env record words
 enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, ENV_FAIL = 5, ENV_VOID = 6 };
-// spawn-ahead status (env word ENV_SPAWN)
+// spawn-ahead status (env word ENV_SPAWN bits 0-1; bits 2-31: the record's
+// generation, bumped by every k_logic draw that voids it)
 enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2, SPAWN_INPROG = 3 };
 
 // Everything a kernel needs, by value (a kernel argument).
@@ -76,6 +83,9 @@ struct KCfg {
     int spawn_budget;           // spawn-ahead time slice per step, s_memrealtime ticks (100 MHz); 0 = none
     int draws_stride;           // u16 entries per env in st.spawn_draws (0: attempts are not sliced)
     int enc_per_wave;           // envs per k_encode wave (1: k_encode, else k_encode_multi with prefetch)
+    int bg;                     // 1: spawn-ahead jobs in the background kernel k_spawn (not k_autoreset)
+    int qpar;                   // queue set of this step (0 unless bg)
+    int spawn_slots;            // k_spawn workers
     // lean encode (encode_lean): the frames copied into a zero-bordered LDS image
     // (lp columns / vr rows of padding, pw bytes per row, pframe bytes per frame)
     // so the crop needs no bounds test; unit -> (snake, row, col, frame) by
@@ -96,6 +106,7 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
                  void *stream);
 int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, const snake_out &o,
                 void *stream);
+int wait_background(const snake_state &st, void *stream);
 int launch_render(const KCfg &k, const snake_state &st, const uint8_t *palette, uint8_t *rgb,
                   void *stream);
 

@@ -973,17 +973,17 @@ __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, 
 
 // The MT19937 state a reset of env e starts from: the spawn-ahead record when
 // one exists (the key and position after its recorded attempts), else the
-// env's own. Returns the record status (wave-uniform).
+// env's own. Returns the status word (wave-uniform; the status is its bits 0-1).
 __device__ __forceinline__ int load_reset_mt(const snake_state &st, int64_t e, WaveMT &mt, int lane)
 {
-    const int spst = st.env[e * kEnvRec + ENV_SPAWN];
-    if (spst != SPAWN_NONE) {
+    const int spw = st.env[e * kEnvRec + ENV_SPAWN];
+    if ((spw & 3) != SPAWN_NONE) {
         const uint32_t *rec = st.spawn + e * kSpawnStride;
         mt_load(mt, rec, (int)rec[kSpawnPos], lane);
     } else {
         mt_load(mt, st.mt + e * kMtN, st.env[e * kEnvRec + ENV_MTPOS], lane);
     }
-    return spst;
+    return spw;
 }
 
 // ------------------------------------------------------------------- reset
@@ -995,8 +995,9 @@ __device__ __forceinline__ int load_reset_mt(const snake_state &st, int64_t e, W
 // record continues the retries where the record left them.
 template <int MS, bool JL, bool SLICE>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
-                         WaveMT &mt, uint8_t *lds, int slot, int spst, int lane, int ps = -1)
+                         WaveMT &mt, uint8_t *lds, int slot, int spw, int lane, int ps = -1)
 {
+    const int spst = spw & 3;
     RPROF_VAL(ps, 4, spst, lane);
     uint8_t *frames = lds + c.lds_frames;
     int *org = reinterpret_cast<int *>(lds + c.lds_centers);
@@ -1076,7 +1077,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         int4 er;
         er.x = S; er.y = 0; er.z = c.fs - 1; er.w = mt.pos;
         *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = er;
-        if (spst != SPAWN_NONE) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = SPAWN_NONE;   // record used up
+        if (spst != SPAWN_NONE) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spw & ~3;   // record used up
         st.env[(int64_t)e * kEnvRec + ENV_FAIL] = failed ? 1 : 0;
         st.env[(int64_t)e * kEnvRec + ENV_VOID] = 0;
         if (failed && o.err) o.err[e] = 2;
@@ -1147,8 +1148,11 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // per-env respawn scratch: G * kRespawnT tempered raws, G chosen cells
     uint32_t *rawbuf = reinterpret_cast<uint32_t *>(lds + E * stride + 2 * kMaxFruits) + g * (G * kRespawnT);
     uint16_t *cellbuf = reinterpret_cast<uint16_t *>(lds + E * stride + 2 * kMaxFruits + E * G * kRespawnT * 4) + g * G;
-    // queue counters (zero between steps: the last k_autoreset worker re-zeroes them)
-    int *qcnt = st.resetq + kNumQ * kQShards * c.q_cap;
+    // this step's queue set and its counters (zero between steps: the last
+    // k_autoreset worker re-zeroes them; the spawn counters of a background
+    // step, the next step's k_autoreset)
+    int *qb = st.resetq + (int64_t)c.qpar * (kNumQ * kQShards * c.q_cap + kQCounters);
+    int *qcnt = qb + kNumQ * kQShards * c.q_cap;
     LSTAMP(40);
     auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
@@ -1163,7 +1167,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
 #ifndef SNAKE_VOID
 #define SNAKE_VOID 1
 #endif
-    const int spst = er2.x, voided = SNAKE_VOID ? er2.z : 0;   // ENV_SPAWN, ENV_VOID
+    const int spst = er2.x & 3, voided = SNAKE_VOID ? er2.z : 0;   // ENV_SPAWN, ENV_VOID
     int4 rec = make_int4(0, 0, 0, 0);
     int act = 0;
     // the snake's running episode statistics, one 16-byte record (snake_epi_stat)
@@ -1546,7 +1550,11 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     }
     // a draw from the MT state voids the env's spawn-ahead record
     const bool drew = mt_slow || mtpos_new != mtpos;
-    const int spst1 = drew ? SPAWN_NONE : spst;
+    // (a draw bumps the record's generation: a background attempt started from the
+    // old state (k_spawn) then fails its final compare-and-swap, or, if that landed
+    // first, is overwritten here; so with bg every draw writes the word)
+    const bool spw_wr = drew && (c.bg || spst != SPAWN_NONE);
+    const uint32_t spw1 = drew ? (((uint32_t)er2.x >> 2) + 1u) << 2 : (uint32_t)er2.x;
     const int voided1 = (drew && spst != SPAWN_NONE) ? 1 : voided;   // (a record was wasted this episode)
 
     LSTAMP(45);
@@ -1569,17 +1577,19 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     LSTAMP(48);
     if (qm) {            // queue the auto-resets in the slots claimed above
         const int base = bcast(qbase, 0);
-        if ((qm >> lane) & 1ull) st.resetq[shard * c.q_cap + base + mbcnt64(qm)] = e;
+        if ((qm >> lane) & 1ull) qb[shard * c.q_cap + base + mbcnt64(qm)] = e;
     }
-    if (pm) {            // and the spawn-ahead jobs
+    // and the spawn-ahead jobs (background: with the generation they were queued at)
+    const int pent = c.bg ? (int)((uint32_t)e | ((spw1 >> 2) << (32 - kQGenBits))) : e;
+    if (pm) {
         const int base = bcast(pbase, 0);
-        if ((pm >> lane) & 1ull) st.resetq[(kQShards + shard) * c.q_cap + base + mbcnt64(pm)] = e;
+        if ((pm >> lane) & 1ull) qb[(kQShards + shard) * c.q_cap + base + mbcnt64(pm)] = pent;
     }
     if (pn) {
         const int base = bcast(nbase, 0);
-        if ((pn >> lane) & 1ull) st.resetq[(2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn)] = e;
+        if ((pn >> lane) & 1ull) qb[(2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn)] = pent;
     }
-    if (env_ok && k == 0 && !bad && spst1 != spst) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spst1;
+    if (env_ok && k == 0 && !bad && spw_wr) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)spw1;
     if (SNAKE_VOID && env_ok && k == 0 && !bad && voided1 != voided) st.env[(int64_t)e * kEnvRec + ENV_VOID] = voided1;
     LSTAMP(49);
     int rank = 1;
@@ -1640,9 +1650,11 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
 // attempt of its next reset, from its MT state or its partial record, into the
 // record. k_logic queues only envs with no ready record whose reset is not this
 // step, so nothing else touches the env's MT state or record meanwhile.
+// The status word spw is the one the attempt started under (generation kept);
+// a background job publishes with a compare-and-swap against it (k_spawn).
 template <int MS>
 __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, const WaveMT &mt, bool ok,
-                                   const int (&q)[MS], int lane)
+                                   const int (&q)[MS], int lane, uint32_t spw, bool cas = false)
 {
     uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
     mt_store(mt, rec, lane);
@@ -1652,7 +1664,10 @@ __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, 
     if (ok && lane < c.S) rec[kSpawnSel + lane] = (uint32_t)mine;
     if (lane == 0) {
         rec[kSpawnPos] = (uint32_t)mt.pos;
-        st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = ok ? SPAWN_READY : SPAWN_PARTIAL;
+        const uint32_t w1 = (spw & ~3u) | (ok ? SPAWN_READY : SPAWN_PARTIAL);
+        uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN);
+        if (cas) atomicCAS(wp, spw, w1);
+        else *wp = w1;
     }
 }
 
@@ -1666,7 +1681,7 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
                          unsigned long long deadline, int lane)
 {
     WaveMT mt;
-    const int spst = load_reset_mt(st, e, mt, lane);
+    const int spw = load_reset_mt(st, e, mt, lane), spst = spw & 3;
     if (spst == SPAWN_READY) return;
     uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
     const int i0 = spst == SPAWN_INPROG ? (int)rec[kSpawnI] : -1;
@@ -1679,11 +1694,36 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
         if (lane == 0) {
             rec[kSpawnPos] = (uint32_t)mt.pos;
             rec[kSpawnI] = (uint32_t)pi;
-            st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = SPAWN_INPROG;
+            st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (spw & ~3) | SPAWN_INPROG;
         }
         return;
     }
-    store_spawn_record<MS>(c, st, e, mt, ok, q, lane);
+    store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)spw);
+}
+
+// Background spawn-ahead job (k_spawn) of env e, queued by the step's k_logic at
+// generation qgen. It runs beside the next step's k_logic, which may draw from
+// the env's MT state meanwhile: such a draw bumps the generation, so a job that
+// sees another generation has nothing to do, and one that read a state being
+// redrawn publishes only if its compare-and-swap still finds qgen's word (if
+// k_logic's store lands after it, that store voids the record). The record is
+// read by the next step's resets only after this kernel has ended.
+template <int MS>
+__device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_t qgen, uint8_t *lds, int lane)
+{
+    const uint32_t spw = __hip_atomic_load(reinterpret_cast<const uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (((spw >> 2) & ((1u << kQGenBits) - 1u)) != qgen || (spw & 3u) == SPAWN_READY) return;
+    WaveMT mt;
+    if ((spw & 3u) != SPAWN_NONE) {
+        const uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
+        mt_load(mt, rec, (int)rec[kSpawnPos], lane);
+    } else {
+        mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
+    }
+    int q[MS], cell;
+    const bool ok = spawn_attempt<MS, true>(c, st, mt, lds, 0, e, 0, q, cell, lane);
+    store_spawn_record<MS>(c, st, e, mt, ok, q, lane, spw, true);
 }
 
 // Spawn-ahead right after an explicit reset (k_reset): the next episode's spawn
@@ -1702,7 +1742,7 @@ __device__ void spawn_after_reset(const KCfg &c, const snake_state &st, int e, W
     bool ok = false;
     for (int a = 0; a < kResetAheadTries && !ok; a++)
         ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, a, q, cell, lane);
-    store_spawn_record<MS>(c, st, e, mt, ok, q, lane);
+    store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)st.env[(int64_t)e * kEnvRec + ENV_SPAWN]);
 }
 
 // ---------------------------------------------------- step: the observation
@@ -1730,7 +1770,9 @@ __device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st,
     encode_obs(c, frames, org, cur + 1 == fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lds, lane);
 }
 
-template <int MS, bool SLICE>
+// RO: resets only (every-step mode, background spawn-ahead): no spawn-job path,
+// fewer registers.
+template <int MS, bool SLICE, bool RO = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KCfg c, const snake_state st, const snake_out o)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1741,7 +1783,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         SLICE ? __builtin_amdgcn_s_memrealtime() + (unsigned long long)c.spawn_budget : 0ull;
     // the shard counts of the three queues, prefix-summed: queue index j lives
     // in the shard whose [excl, incl) holds it
-    int *qc = st.resetq + kNumQ * kQShards * c.q_cap;
+    const int64_t qset = kNumQ * kQShards * c.q_cap + kQCounters;
+    int *qb = st.resetq + c.qpar * qset;
+    int *qc = qb + kNumQ * kQShards * c.q_cap;
+    if (c.bg && blockIdx.x == 0) {
+        // the other set's spawn counters: its k_spawn (the last step's) has ended
+        // (launch_step orders this kernel after it) and the next step that fills
+        // them (k_logic, after this kernel) has not begun
+        int *oc = st.resetq + (1 - c.qpar) * qset + kNumQ * kQShards * c.q_cap;
+        for (int q = kQShards + lane; q < kNumQ * kQShards; q += kWave) oc[q * kQSpread] = 0;
+        if (lane < kClaimShards) oc[(kQSpClaim + lane) * kQSpread] = 0;
+    }
     const int cnt = qc[lane * kQSpread], ucnt = qc[(kQShards + lane) * kQSpread],
               ncnt = qc[(2 * kQShards + lane) * kQSpread];
     const int incl = wave_scan(cnt, lane), uincl = wave_scan(ucnt, lane), nincl = wave_scan(ncnt, lane);
@@ -1753,7 +1805,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     // of workers reaches; their envs are queued again next step
     int Nn = bcast(nincl, kWave - 1);
     if (c.spawn_cap) Nn = min(Nn, max(G - R - U, 0));
-    const int P = U + Nn;
+    const int P = (RO || c.bg) ? 0 : U + Nn;   // (background: the spawn jobs are k_spawn's)
     const int T = R + P;
     if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
     // env of job j of queue q
@@ -1762,7 +1814,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     auto job_env = [&](int q, int j, int qincl) {
         const int sh = __popcll(__ballot(qincl <= j));
         const int base = sh ? bcast(qincl, sh - 1) : 0;
-        return st.resetq[(q * kQShards + sh) * c.q_cap + j - base];
+        return qb[(q * kQShards + sh) * c.q_cap + j - base];
     };
     // job idx < R: the step's resets (high priority, the critical path); then
     // the urgent spawn-ahead jobs, then the others. A worker's first job is its
@@ -1776,13 +1828,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             const int e = job_env(0, idx, incl);
             WaveMT mt;
             const int spst = load_reset_mt(st, e, mt, lane);
-            if (c.diag && lane == 0 && spst == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
+            if (c.diag && lane == 0 && (spst & 3) == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
             if (idx < 128) OBSPROF(idx, lane);
             const int ps = idx < 128 ? idx : -1;
             if (c.link_in_lds) do_reset<MS, true, SLICE>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
             else do_reset<MS, false, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
             if (idx < 128) OBSPROF(128 + idx, lane);
-        } else if (idx < R + P) {
+        } else if (!RO && idx < R + P) {
             if (c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
             else if (c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(2);
@@ -1814,8 +1866,49 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     if (nx == jobs_x + workers_x - 1) {
         int d = 0;
         if (lane == 0) d = atomicAdd(&qc[kQDone * kQSpread], 1);
-        if (bcast(d, 0) == nsh - 1)
-            for (int q = lane; q < kQCount; q += kWave) qc[q * kQSpread] = 0;
+        if (bcast(d, 0) == nsh - 1)   // (background: the reset counters only)
+            for (int q = lane; q < kQCount; q += kWave)
+                if (!c.bg || q < kQShards || (q >= kQClaim && q <= kQDone)) qc[q * kQSpread] = 0;
+    }
+}
+
+// Background spawn-ahead (KCfg.bg): the step's spawn-ahead jobs, run by
+// spawn_slots one-wave workers on a stream of their own that the step does not
+// join -- beside the step's resets and encodes and the next step's k_logic; the
+// next step's k_autoreset waits for it (launch_step). Jobs are claimed on 16
+// claim shards like k_autoreset's; the counters are re-zeroed by the next
+// step's k_autoreset.
+template <int MS>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_spawn(const KCfg c, const snake_state st)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    if (c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
+    else if (c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(2);
+    int *qb = st.resetq + (int64_t)c.qpar * (kNumQ * kQShards * c.q_cap + kQCounters);
+    int *qc = qb + kNumQ * kQShards * c.q_cap;
+    const int ucnt = qc[(kQShards + lane) * kQSpread], ncnt = qc[(2 * kQShards + lane) * kQSpread];
+    const int uincl = wave_scan(ucnt, lane), nincl = wave_scan(ncnt, lane);
+    const int U = bcast(uincl, kWave - 1), T = U + bcast(nincl, kWave - 1);
+    const int G = (int)gridDim.x, nsh = min(G, kClaimShards);
+    const int x = G >= kClaimShards ? (int)(blockIdx.x & (kClaimShards - 1)) : (int)blockIdx.x % nsh;
+    auto job_env = [&](int q, int j, int qincl) {
+        const int sh = __popcll(__ballot(qincl <= j));
+        const int base = sh ? bcast(qincl, sh - 1) : 0;
+        return qb[(q * kQShards + sh) * c.q_cap + j - base];
+    };
+    for (int idx = blockIdx.x; idx < T;) {
+        const int ent = idx < U ? job_env(1, idx, uincl) : job_env(2, idx - U, nincl);
+        const int e = ent & ((1 << (32 - kQGenBits)) - 1);
+        const uint32_t qgen = (uint32_t)ent >> (32 - kQGenBits);
+        if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
+        if (idx < 128) OBSPROF(512 + idx, lane);
+        do_spawn_bg<MS>(c, st, e, qgen, lds, lane);
+        if (idx < 128) OBSPROF(640 + idx, lane);
+        int v = 0;
+        if (lane == 0) v = atomicAdd(&qc[(kQSpClaim + x) * kQSpread], 1);
+        idx = G + x + nsh * bcast(v, 0);
     }
 }
 
@@ -2140,12 +2233,62 @@ static int check_launch(const char *what)
     return SNAKE_OK;
 }
 
+// The fork/join events only order kernels of one device: no system-scope fence
+// (that would write the L2s back for a host that never looks). Stream
+// write/wait-value packets on signal memory were tried for the fork/join and
+// measured no faster in the step (scripts/microbench/forkjoin.hip shows them
+// cheaper in isolation).
+constexpr unsigned kJoinFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+
+// Background spawn-ahead (KCfg.bg) per state (keyed by its env records): the
+// stream k_spawn runs on, the event recorded after the last one, the step
+// counter whose parity picks the queue set.
+struct BgCtx {
+    hipStream_t x = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t steps = 0;
+    bool pending = false;
+};
+static std::mutex g_bgmu;
+static std::map<const void *, BgCtx> g_bg;
+
+static BgCtx *bg_ctx(const snake_state &st, bool create)
+{
+    std::lock_guard<std::mutex> g(g_bgmu);
+    auto it = g_bg.find(st.env);
+    if (it != g_bg.end()) return &it->second;
+    if (!create) return nullptr;
+    BgCtx c;
+    static const char *ev_sp = getenv("SNAKE_BG_STREAM_PRIO");   // 1: the lowest stream priority
+    int least = 0, greatest = 0;
+    if (ev_sp && atoi(ev_sp)) hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (hipStreamCreateWithPriority(&c.x, hipStreamNonBlocking, least) != hipSuccess ||
+        hipEventCreateWithFlags(&c.done, kJoinFlags) != hipSuccess) {
+        set_error("background stream / event creation failed");
+        return nullptr;
+    }
+    return &g_bg.emplace(st.env, c).first->second;   // (std::map: the address stays valid)
+}
+
+// `stream` waits for the state's last background spawn kernel (if any).
+int wait_background(const snake_state &st, void *stream)
+{
+    BgCtx *b = bg_ctx(st, false);
+    if (!b || !b->pending) return SNAKE_OK;
+    if (hipStreamWaitEvent((hipStream_t)stream, b->done, 0) != hipSuccess) {
+        set_error("waiting for the background spawn kernel failed");
+        return SNAKE_E_LAUNCH;
+    }
+    return SNAKE_OK;
+}
+
 int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_t env_offset,
                 void *stream)
 {
     const int threads = 256, blocks = (k.N + threads - 1) / threads;
     DeviceGuard dg((hipStream_t)stream);
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
+    if (int rc = wait_background(st, stream)) return rc;
     hipLaunchKernelGGL(k_seed, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, k, st,
                        base_seed, (long long)env_offset);
     return check_launch("k_seed");
@@ -2172,6 +2315,7 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
     const dim3 grid(k.link_in_lds ? k.N : k.reset_slots), block(kWave);
     DeviceGuard dg((hipStream_t)stream);
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
+    if (int rc = wait_background(st, stream)) return rc;
     TimedLaunch tl("k_reset", (hipStream_t)stream);
     if (k.S <= 4) hipLaunchKernelGGL(k_reset<4>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
     else if (k.S <= 8) hipLaunchKernelGGL(k_reset<8>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
@@ -2187,12 +2331,6 @@ struct SideCtx {
     hipEvent_t fork, join;
 };
 
-// The fork/join events only order kernels of one device: no system-scope fence
-// (that would write the L2s back for a host that never looks). Stream
-// write/wait-value packets on signal memory were tried for the fork/join and
-// measured no faster in the step (scripts/microbench/forkjoin.hip shows them
-// cheaper in isolation).
-constexpr unsigned kJoinFlags = hipEventDisableTiming | hipEventDisableSystemFence;
 
 static int side_ctx(hipStream_t main, int dev, SideCtx *out)
 {
@@ -2225,6 +2363,11 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     const int ms = k.S <= 4 ? 4 : (k.S <= 8 ? 8 : 16), epw = kWave / ms;   // envs per k_logic wave
     const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits + epw * ms * kRespawnT * 4 + epw * ms * 2;
     const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
+    BgCtx *bgc = nullptr;
+    if (k.bg) {   // background spawn-ahead: this step's queue set
+        if (!(bgc = bg_ctx(st, true))) return SNAKE_E_LAUNCH;
+        k.qpar = (int)(bgc->steps & 1);
+    }
     TimedLaunch t1("k_logic", sm);
     if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, k, st, actions, o);
     else if (ms == 8) hipLaunchKernelGGL(k_logic<8>, gl, block, lds_logic, sm, k, st, actions, o);
@@ -2235,9 +2378,9 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     if (k.autoreset == 2) {   // every env resets (the resets write the obs), then the
                               // encodes of the envs rejected for an invalid action
         TimedLaunch t2("k_autoreset", sm);
-        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false>), gr, block, k.lds_bytes, sm, k, st, o);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false>), gr, block, k.lds_bytes, sm, k, st, o);
-        else hipLaunchKernelGGL((k_autoreset<16, false>), gr, block, k.lds_bytes, sm, k, st, o);
+        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false, true>), gr, block, k.lds_bytes, sm, k, st, o);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false, true>), gr, block, k.lds_bytes, sm, k, st, o);
+        else hipLaunchKernelGGL((k_autoreset<16, false, true>), gr, block, k.lds_bytes, sm, k, st, o);
         t2.close();
         if ((rc = check_launch("k_autoreset"))) return rc;
         TimedLaunch t3("k_encode", sm);
@@ -2262,6 +2405,31 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         set_error("fork to the side stream failed");
         return SNAKE_E_LAUNCH;
     }
+    if (bgc) {
+        // the resets after the last step's spawn kernel (its records), this
+        // step's spawn kernel on the background stream, not joined
+        if ((bgc->pending && hipStreamWaitEvent(sm, bgc->done, 0) != hipSuccess) ||
+            hipStreamWaitEvent(bgc->x, sc.fork, 0) != hipSuccess) {
+            set_error("ordering the background spawn kernel failed");
+            return SNAKE_E_LAUNCH;
+        }
+        KCfg ks = k;
+        ks.lds_link = 0;   // (only the draw record)
+        const int lds_sp = (int)(((int64_t)2 * (k.n_cand + kWave) + 15) / 16 * 16);
+        const dim3 gs(k.spawn_slots);
+        TimedLaunch t4("k_spawn", bgc->x);
+        if (k.S <= 4) hipLaunchKernelGGL(k_spawn<4>, gs, block, lds_sp, bgc->x, ks, st);
+        else if (k.S <= 8) hipLaunchKernelGGL(k_spawn<8>, gs, block, lds_sp, bgc->x, ks, st);
+        else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bgc->x, ks, st);
+        t4.close();
+        if ((rc = check_launch("k_spawn"))) return rc;
+        if (hipEventRecord(bgc->done, bgc->x) != hipSuccess) {
+            set_error("background spawn event failed");
+            return SNAKE_E_LAUNCH;
+        }
+        bgc->pending = true;
+        bgc->steps++;
+    }
     static const bool resets_main = !(getenv("SNAKE_ENCODE_ON_MAIN") && atoi(getenv("SNAKE_ENCODE_ON_MAIN")));
     const hipStream_t s_res = resets_main ? sm : sc.side, s_enc = resets_main ? sc.side : sm;
     auto launch_resets = [&]() {
@@ -2272,6 +2440,10 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
             if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true>), gr, block, k.lds_bytes, s_res, k, st, o);
             else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true>), gr, block, k.lds_bytes, s_res, k, st, o);
             else hipLaunchKernelGGL((k_autoreset<16, true>), gr, block, k.lds_bytes, s_res, k, st, o);
+        } else if (k.bg) {
+            if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false, true>), gr, block, k.lds_bytes, s_res, k, st, o);
+            else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false, true>), gr, block, k.lds_bytes, s_res, k, st, o);
+            else hipLaunchKernelGGL((k_autoreset<16, false, true>), gr, block, k.lds_bytes, s_res, k, st, o);
         } else {
             if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false>), gr, block, k.lds_bytes, s_res, k, st, o);
             else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false>), gr, block, k.lds_bytes, s_res, k, st, o);

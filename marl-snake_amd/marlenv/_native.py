@@ -10,11 +10,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 12
+SNAKE_ABI_VERSION = 13
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
-           'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version',
+           'snake_sync', 'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version',
            'snake_dqn_plan', 'snake_dqn_rows', 'snake_dqn_forward', 'snake_dqn32_scratch', 'snake_dqn32_forward')
 
 
@@ -27,7 +27,7 @@ class SnakeCfg(ctypes.Structure):
                 ('rew_lose', ctypes.c_double), ('rew_win', ctypes.c_double),
                 ('rew_time', ctypes.c_double), ('max_episode_steps', ctypes.c_double),
                 ('coop', ctypes.c_int32), ('autoreset', ctypes.c_int32), ('spawn_ahead', ctypes.c_int32),
-                ('spawn_budget_us', ctypes.c_int32)]
+                ('spawn_budget_us', ctypes.c_int32), ('spawn_background', ctypes.c_int32)]
 
 
 class SnakeLayout(ctypes.Structure):
@@ -106,6 +106,7 @@ def lib(path=None):
                               ctypes.POINTER(SnakeOut), P]
     L.snake_step.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P,
                              ctypes.POINTER(SnakeOut), P]
+    L.snake_sync.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P]
     L.snake_render_rgb.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P, P, P]
     L.snake_dqn_plan.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(DqnLayout)]
     L.snake_dqn_rows.argtypes = [ctypes.POINTER(DqnCfg), P, I64]

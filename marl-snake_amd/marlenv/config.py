@@ -41,6 +41,8 @@ def build_cfg(height=20, width=20, num_snakes=4, snake_length=3, vision_range=No
     spawn_ahead = int(kwargs.pop('spawn_ahead', 0))
     # time slice of the spawn-ahead attempts per step, us (0 automatic, -1 unlimited)
     spawn_budget_us = int(kwargs.pop('spawn_budget_us', 0))
+    # spawn-ahead attempts in a background kernel (0 automatic, 1 on, -1 off)
+    spawn_background = int(kwargs.pop('spawn_background', 0))
     num_fruits = kwargs.pop('num_fruits', int(round(num_snakes * 0.8)))
     if observer not in ('snake', 'human'):
         raise ValueError(f"observer must be 'snake' or 'human' (got {observer!r})")
@@ -49,7 +51,7 @@ def build_cfg(height=20, width=20, num_snakes=4, snake_length=3, vision_range=No
         int(frame_stack), 1 if observer == 'human' else 0, int(num_fruits),
         float(reward_dict['fruit']), float(reward_dict['kill']), float(reward_dict['lose']),
         float(reward_dict['win']), float(reward_dict['time']), float(max_episode_steps),
-        1 if coop else 0, autoreset_code(autoreset), spawn_ahead, spawn_budget_us)
+        1 if coop else 0, autoreset_code(autoreset), spawn_ahead, spawn_budget_us, spawn_background)
     meta = dict(height=int(height), width=int(width), num_snakes=int(num_snakes),
                 snake_length=int(snake_length), vision_range=vision_range,
                 frame_stack=int(frame_stack), observer=observer, reward_dict=reward_dict,

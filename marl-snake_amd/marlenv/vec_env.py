@@ -42,6 +42,12 @@ def _current_device():
     return torch._C._cuda_getDevice()
 
 
+def torch_cuda_alive():
+    """False during interpreter shutdown (no library calls from finalizers then)."""
+    import sys
+    return not sys.is_finalizing()
+
+
 _INFO_KEYS = ('episode_done', 'rank', 'episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills',
               'error')
 
@@ -167,6 +173,15 @@ class SnakeVecEnv:
     # ------------------------------------------------------------------ utils
     def _stream(self):
         return ctypes.c_void_p(_raw_stream(self._dev_index))
+
+    def sync(self):
+        """Order the current stream after the background spawn-ahead kernel of
+        the last step (include/snake_env.h snake_sync): call before reading or
+        writing the state buffers directly. The methods here that touch state do."""
+        torch = _torch()
+        with torch.cuda.device(self.device):
+            check(self._L.snake_sync(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
+                                     self._stream()))
 
     # Outputs of one call (include/snake_env.h snake_out): the observations in a
     # fresh allocation of their own (a bare observation buffer that the caller
@@ -332,13 +347,14 @@ class SnakeVecEnv:
         (train_dqn.py:356-383)."""
         torch = _torch()
         dev = torch.device(device) if device is not None else self.device
+        self.sync()
         torch.cuda.current_stream(self.device).synchronize()
         sd = {k: getattr(self, k).detach().to(dev, copy=True) for k in self._STATE_BUFFERS}
         # a paused spawn-ahead attempt keeps its draws in spawn_draws, which is not
         # saved: the snapshot marks it as no record (spawn-ahead never changes
         # results, the attempt is simply redone)
         er = sd['env_rec'].view(self.num_envs, 8)
-        er[:, 4].masked_fill_(er[:, 4] == 3, 0)
+        er[:, 4].masked_fill_((er[:, 4] & 3) == 3, 0)
         sd['meta'] = self._snapshot_meta()
         return sd
 
@@ -359,6 +375,7 @@ class SnakeVecEnv:
         for key in ('abi', 'num_envs', 'cfg', 'sizes'):
             if mine[key] != theirs[key]:
                 raise ValueError(f'snapshot does not match this env: {key} {theirs[key]} != {mine[key]}')
+        self.sync()
         with torch.cuda.device(self.device):
             for k in self._STATE_BUFFERS:
                 getattr(self, k).copy_(sd[k].to(self.device))
@@ -390,6 +407,7 @@ class SnakeVecEnv:
         """Overwrite env i's MT19937 key (624 uint32, as int32) and position; voids
         its spawn-ahead record (include/snake_env.h), which was drawn from the old state."""
         torch = _torch()
+        self.sync()
         er = self.env_rec.view(self.num_envs, 8)
         self.mt.view(self.num_envs, 624)[i].copy_(torch.as_tensor(key).to(self.device))
         er[i, 3] = int(pos)
@@ -402,6 +420,7 @@ class SnakeVecEnv:
         stack is refilled with this grid and the episode statistics are zeroed, as
         _init_obs/_reset_epi_stats do; the env's MT19937 stream is left as is."""
         torch = _torch()
+        self.sync()
         H, W = self.grid_shape
         S, fs, lay = self.num_snakes, self.cfg.frame_stack, self.layout
         g = np.zeros(lay.grid_stride, np.uint8)
@@ -439,4 +458,13 @@ class SnakeVecEnv:
         self._reset_done = True
 
     def close(self):
-        pass
+        # the state buffers go back to the allocator on the current stream: order
+        # that after a background spawn kernel still writing them
+        if getattr(self, '_state', None) is not None and torch_cuda_alive():
+            try:
+                self.sync()
+            except Exception:
+                pass
+
+    def __del__(self):
+        self.close()

@@ -79,7 +79,7 @@ def main():
             'spawn_dur_us': pct((se[sok] - ss[sok]) / 100.0) if sok.any() else None,
             # per reset: status at start (0 none, 1 partial, 2 ready, 3 in progress) and the
             # phase durations: poses, paint, fruits, grid/key stores, encode
-            'reset_phases_us': [[int(p[4])] + [round(float(x), 1) for x in np.diff(
+            'reset_phases_us': [[int(p[4]) & 3] + [round(float(x), 1) for x in np.diff(
                 np.array([r, p[0], p[1], p[2], p[3], en], dtype=np.int64)) / 100.0]
                 for r, p, en in zip(rs, ph, re_)][:12],
         }), flush=True)
