@@ -98,7 +98,7 @@ typedef struct {
     int64_t spawn_draws;/* uint16 [N][round8(n_cand)]    draws of paused spawn-ahead attempts (j_i at
                                                          index i); 0 when attempts are not sliced
                                                          (spawn-ahead off, or global link tables) */
-    int64_t resetq;     /* int32  2 x ([3][64][cap] + [225*32]) sharded auto-reset and spawn-ahead
+    int64_t resetq;     /* int32  2 x ([3][64][cap] + [226*32]) sharded auto-reset and spawn-ahead
                                                          queues + the step's counters, one per 128-B
                                                          line; two sets, by step parity (zero-initialised) */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */

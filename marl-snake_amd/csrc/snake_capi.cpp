@@ -261,6 +261,38 @@ static int64_t spawn_budget_us(const snake_cfg *c, int64_t n_cand, int64_t N = 0
     return us;
 }
 
+// spawn-ahead threshold: by default envs with at most 2 live snakes
+// (any env under coop, where one death ends the episode); -1 = off
+static int spawn_thr_of(const snake_cfg *c)
+{
+    static const char *ev = getenv("SNAKE_SPAWN_THR");
+    int thr;
+    if (c->spawn_ahead != 0) thr = c->spawn_ahead < 0 ? -1 : c->spawn_ahead;
+    else thr = ev ? atoi(ev) : (c->coop ? c->num_snakes : 2);
+    if (c->autoreset != 1) thr = -1;   // (every-step resets: nothing to draw ahead)
+    return thr;
+}
+
+// Background spawn-ahead (snake_kernels.hip k_spawn): the attempts leave the
+// step entirely (the step never waits for them; two steps later its k_logic
+// does, for the queue set). Needs spawn-ahead on (all-done auto-reset),
+// unsliced attempts and the draw record in LDS. cfg->spawn_background: 0
+// automatic (SNAKE_BG overrides), 1 on, -1 off. Automatic: boards of more than
+// 8192 spawn poses, whose attempt outlasts a step (40x40: ~110 us); at 20x20
+// the background jobs slowed the concurrent encodes more than they saved
+// (cfg3 0.111 -> 0.124 ms with the one-step wait).
+static bool bg_of(const snake_cfg *c, int64_t n_cand)
+{
+    static const char *ev_bg = getenv("SNAKE_BG");
+#ifndef SNAKE_BG_DEFAULT
+#define SNAKE_BG_DEFAULT 1
+#endif
+    const bool want = c->spawn_background != 0 ? c->spawn_background > 0
+                                                : (ev_bg ? atoi(ev_bg) != 0 : (SNAKE_BG_DEFAULT && n_cand > 8192));
+    return want && spawn_thr_of(c) >= 0 && spawn_budget_us(c, n_cand) <= 0 &&
+           2 * (n_cand + kWave) <= kJarrLdsMax;
+}
+
 int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
 {
     int rc = check_cfg(c);
@@ -291,7 +323,8 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     // global u32 link table per reset worker.
     const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
     o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
-    o->spawn = N * kSpawnStride * 4;
+    // (background spawn-ahead: two records per env, see k_spawn)
+    o->spawn = (bg_of(c, o->n_cand) ? 2 : 1) * N * kSpawnStride * 4;
     // paused spawn-ahead attempts keep their draws here (u16 per draw index):
     // only where attempts are sliced (spawn_budget_us) -- spawn-ahead on
     // (all-done auto-reset), the draw record in LDS -- and below 32 GiB
@@ -399,9 +432,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->spawn_prio = ev_prio ? std::max(0, std::min(3, atoi(ev_prio))) : 1;
     // k_encode above the spawn-ahead jobs: the bandwidth-bound encodes then keep
     // HBM busy while the compute-bound workers fill the issue gaps (SNAKE_ENCODE_PRIO,
-    // default 2: step 0.1275 -> 0.1200 ms at cfg3; 0 = hardware default)
+    // default 2: step 0.1275 -> 0.1200 ms at cfg3; 0 = hardware default). With
+    // background spawn-ahead (set below) the step's resets are the critical path
+    // beside the encodes instead: default 0 (cfg5 0.160 -> 0.135 ms).
     static const char *ev_eprio = getenv("SNAKE_ENCODE_PRIO");
-    k->encode_prio = ev_eprio ? std::max(0, std::min(3, atoi(ev_eprio))) : 2;
+    k->encode_prio = ev_eprio ? std::max(0, std::min(3, atoi(ev_eprio))) : (bg_of(c, n_cand) ? 0 : 2);
     // SNAKE_SPAWN_CAP=1: the other (2-live-snake) spawn-ahead jobs past the
     // workers' first round wait for a later step (the urgent ones never do);
     // off by default: measured 0.121 vs 0.109 ms at cfg3 (the hit rate falls)
@@ -417,12 +452,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         const int64_t blocks = (N + k->q_envs_per_block - 1) / k->q_envs_per_block;
         k->q_cap = (int)((blocks + kQShards - 1) / kQShards * k->q_envs_per_block);
     }
-    // spawn-ahead: by default envs with at most 2 live snakes (any env
-    // under coop, where one death ends the episode); -1 = off
-    static const char *ev = getenv("SNAKE_SPAWN_THR");
-    if (c->spawn_ahead != 0) k->spawn_thr = c->spawn_ahead < 0 ? -1 : c->spawn_ahead;
-    else k->spawn_thr = ev ? atoi(ev) : (k->coop ? k->S : 2);
-    if (k->autoreset != 1) k->spawn_thr = -1;   // (every-step resets: nothing to draw ahead)
+    k->spawn_thr = spawn_thr_of(c);
     // spawn-ahead time slice (spawn_budget_us above)
     k->draws_stride = lay.spawn_draws ? (int)round_up(lay.n_cand, 8) : 0;
     {
@@ -434,27 +464,17 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         k->spawn_budget = (SNAKE_SLICE && us > 0 && k->draws_stride > 0 && k->spawn_thr >= 0)
                               ? (int)std::min<int64_t>(us * 100, 1 << 30) : 0;
     }
-    // background spawn-ahead (snake_kernels.hip k_spawn): the jobs leave the
-    // step's critical window; with spawn-ahead on, all-done auto-reset, the draw
-    // record in LDS (the global link tables are per reset worker) and unsliced
-    // attempts. cfg->spawn_background: 0 automatic (SNAKE_BG overrides), 1 on, -1 off.
-    {
-        static const char *ev_bg = getenv("SNAKE_BG");
-#ifndef SNAKE_BG_DEFAULT
-#define SNAKE_BG_DEFAULT 1
-#endif
-        // automatic: boards of more than 8192 spawn poses, whose attempt outlasts a
-        // step (40x40: ~110 us; cfg5 step 0.149 -> 0.142 ms); at 20x20 the
-        // background jobs slowed the concurrent encodes more than they saved
-        // (cfg3 0.111 -> 0.124, cfg2 0.064 -> 0.065..0.078 ms)
-        const bool want = c->spawn_background != 0 ? c->spawn_background > 0
-                                                    : (ev_bg ? atoi(ev_bg) != 0
-                                                             : (SNAKE_BG_DEFAULT && lay.n_cand > 8192));
-        k->bg = (want && k->spawn_thr >= 0 && k->autoreset == 1 && k->spawn_budget == 0 &&
-                 2 * ((int64_t)lay.n_cand + kWave) <= kJarrLdsMax) ? 1 : 0;
+    {   // background spawn-ahead (bg_of above)
+        k->bg = bg_of(c, lay.n_cand) && k->spawn_budget == 0 ? 1 : 0;
+        if (bg_of(c, lay.n_cand) != (k->bg != 0)) {
+            set_error("background spawn-ahead needs unsliced attempts");
+            return SNAKE_E_CONFIG;
+        }
         static const char *ev_ss = getenv("SNAKE_SPAWN_SLOTS");
         const int ss = ev_ss ? std::max(1, atoi(ev_ss)) : kResetSlots;
         k->spawn_slots = (int)std::min<int64_t>(N, ss);
+        static const char *ev_bt = getenv("SNAKE_BG_TRIES");
+        k->bg_tries = ev_bt ? std::max(1, atoi(ev_bt)) : 1;
     }
     k->lds_obs_bytes = off;
     {   // lean encode (snake_kernels.hip encode_lean): zero-bordered frames in LDS
@@ -474,9 +494,14 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         k->mag_wpr = mag(std::max(1, k->W / 4));
         k->lds_lean_bytes = (int)round_up((int64_t)k->fs * k->pframe, 16) + 4 * k->fs * kMaxSnakes;
         // the reciprocals must be exact for every unit index and grid word
-        // (k_encode_lean: grids with W % 4 == 0, at most 32 prefetched frame dwords per lane)
+        // (k_encode_lean: grids with W % 4 == 0, at most 8 prefetched frame dwords
+        // per thread: one wave per env up to 512 dwords, four up to 2048)
+        static const char *ev_lt = getenv("SNAKE_LEAN_THREADS");
+        const int64_t fdw = (int64_t)k->fs * k->HW / 4;
+        k->lean_threads = fdw <= 8 * kWave ? kWave : 256;
+        if (ev_lt && atoi(ev_lt) == 256) k->lean_threads = 256;
         bool exact = (k->units % 2) == 0 && k->units < (1 << 22) && k->lds_lean_bytes <= 48 * 1024 &&
-                     k->W % 4 == 0 && (int64_t)k->fs * k->HW / 4 <= 8 * kWave;
+                     k->W % 4 == 0 && fdw <= 8 * k->lean_threads;
         for (int64_t u = 0; exact && u < k->units; u++) {
             const int64_t q = ((uint64_t)u * k->mag_ups) >> 32, r0 = u - q * k->ups;
             const int64_t i = ((uint64_t)r0 * k->mag_rowl) >> 32, r1 = r0 - i * k->rowl;
@@ -496,8 +521,8 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
 #define SNAKE_EPW_DEFAULT 2
 #endif
         // (measured: 2 with the lean encode at cfg3/cfg2; one env per wave otherwise)
-        int epw = ev_epw ? atoi(ev_epw) : (k->lean ? SNAKE_EPW_DEFAULT : 1);
-        if (k->ring_bytes > 8 * 1024) epw = 1;
+        int epw = ev_epw ? atoi(ev_epw) : (k->lean ? (k->lean_threads == kWave ? SNAKE_EPW_DEFAULT : 2) : 1);
+        if (k->ring_bytes > 8 * 1024 && !k->lean) epw = 1;
         k->enc_per_wave = std::max(1, std::min(epw, 64));
     }
     // the reset workers never use the encode staging buffer: the draw record

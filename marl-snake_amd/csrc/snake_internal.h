@@ -32,7 +32,8 @@ constexpr int kNumQ = 3;            // queues: 0 resets, 1 urgent spawn-ahead (<
 constexpr int kQClaim = kNumQ * kQShards;             // counter index of claim shard 0
 constexpr int kQDone = kQClaim + kClaimShards;        // counter index: claim shards drained
 constexpr int kQSpClaim = kQDone + 1;                 // background spawn kernel (k_spawn): claim shard 0
-constexpr int kQCount = kQSpClaim + kClaimShards;     // counters
+constexpr int kQSpDone = kQSpClaim + kClaimShards;    // k_spawn: claim shards drained
+constexpr int kQCount = kQSpDone + 1;                 // counters
 constexpr int kQCounters = kQCount * kQSpread;        // words
 // The queues and counters exist twice (the step's parity, KCfg.qpar): with the
 // background spawn kernel a step's spawn-ahead queues are still being read while
@@ -86,11 +87,13 @@ struct KCfg {
     int bg;                     // 1: spawn-ahead jobs in the background kernel k_spawn (not k_autoreset)
     int qpar;                   // queue set of this step (0 unless bg)
     int spawn_slots;            // k_spawn workers
+    int bg_tries;               // k_spawn: permutation attempts per job (until disjoint)
     // lean encode (encode_lean): the frames copied into a zero-bordered LDS image
     // (lp columns / vr rows of padding, pw bytes per row, pframe bytes per frame)
     // so the crop needs no bounds test; unit -> (snake, row, col, frame) by
     // multiply-high reciprocals of ups = oh*ow*fs, rowl = ow*fs, fs, and of W/4
     int lean, lp, pw, pframe, lds_lean_bytes, ups, rowl;
+    int lean_threads;           // threads per lean-encode workgroup (64, or 256 for rings over 512 dwords)
     uint32_t mag_ups, mag_rowl, mag_fs, mag_wpr;
     double rf, rk, rl, rw, rt, max_steps;
 };

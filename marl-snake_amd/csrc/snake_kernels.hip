@@ -751,11 +751,12 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
 // units (8 obs bytes each: one cell of one frame): per unit one LDS byte read
 // and its one-hot channel (_encode :481-492), no LDS staging of the output, no
 // divergent branch.
+template <int T = kWave>
 __device__ void encode_lean(const KCfg &c, const uint8_t *pf, const int *base, int slot0, uint8_t *obs_env,
                             int lane)
 {
     const int pairs = c.units >> 1;
-    for (int p = lane; p < pairs; p += kWave) {
+    for (int p = lane; p < pairs; p += T) {
         const uint32_t u = 2u * (uint32_t)p;
         int kk = (int)__umulhi(u, c.mag_ups);
         const int r0 = (int)u - kk * c.ups;
@@ -821,9 +822,10 @@ __device__ void stage_lean(const KCfg &c, const snake_state &st, int64_t e, uint
     }
 }
 
+template <int T = kWave>
 __device__ __forceinline__ void zero_lean(const KCfg &c, uint8_t *pf, int lane)
 {
-    for (int q = lane; q < (c.fs * c.pframe) >> 4; q += kWave) reinterpret_cast<uint4 *>(pf)[q] = make_uint4(0, 0, 0, 0);
+    for (int q = lane; q < (c.fs * c.pframe) >> 4; q += T) reinterpret_cast<uint4 *>(pf)[q] = make_uint4(0, 0, 0, 0);
 }
 
 // Row-wise encode: lane = one (snake, frame, window row); the row's cells are
@@ -971,15 +973,64 @@ __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, 
     return __ballot(dup) == 0ull;
 }
 
+// Spawn-ahead status word (env word ENV_SPAWN): bits 0-1 the status, bit 2 the
+// record buffer holding the record (background spawn-ahead keeps two per env,
+// k_spawn), bits 3-31 the generation (bumped by every draw that voids it).
+constexpr uint32_t kGenOne = 8;
+__device__ __forceinline__ uint32_t *spawn_rec(const KCfg &c, const snake_state &st, int64_t e, int b)
+{
+    return st.spawn + ((int64_t)b * c.N + e) * kSpawnStride;
+}
+
+// Hand-off of a record between concurrently running kernels (background
+// spawn-ahead): write-through (sc1) stores, drained, then the status word's
+// compare-and-swap; the reader takes the word with an atomic and loads the
+// record with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void mt_load_sc1(WaveMT &m, const uint32_t *g, int pos, int lane)
+{
+#pragma unroll
+    for (int t = 0; t < 10; t++) {
+        const int e = 64 * t + lane;
+        m.w[t] = (e < kMtN) ? ld_sc1(g + e) : 0u;
+    }
+    m.pos = pos;
+}
+
 // The MT19937 state a reset of env e starts from: the spawn-ahead record when
 // one exists (the key and position after its recorded attempts), else the
 // env's own. Returns the status word (wave-uniform; the status is its bits 0-1).
-__device__ __forceinline__ int load_reset_mt(const snake_state &st, int64_t e, WaveMT &mt, int lane)
+__device__ __forceinline__ int load_reset_mt(const KCfg &c, const snake_state &st, int64_t e, WaveMT &mt, int lane)
 {
     const int spw = st.env[e * kEnvRec + ENV_SPAWN];
     if ((spw & 3) != SPAWN_NONE) {
-        const uint32_t *rec = st.spawn + e * kSpawnStride;
+        const uint32_t *rec = spawn_rec(c, st, e, (spw >> 2) & 1);
         mt_load(mt, rec, (int)rec[kSpawnPos], lane);
+    } else {
+        mt_load(mt, st.mt + e * kMtN, st.env[e * kEnvRec + ENV_MTPOS], lane);
+    }
+    return spw;
+}
+
+// Background spawn-ahead (KCfg.bg): an auto-reset takes env e's record with one
+// atomic that bumps the generation (a k_spawn job still working on the env then
+// fails its publish), and reads the record it found with sc1 loads.
+__device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &st, int64_t e, WaveMT &mt,
+                                              int lane)
+{
+    int v = 0;
+    if (lane == 0) v = (int)atomicAdd(reinterpret_cast<uint32_t *>(st.env + e * kEnvRec + ENV_SPAWN), kGenOne);
+    const int spw = __shfl(v, 0);
+    if ((spw & 3) != SPAWN_NONE) {
+        const uint32_t *rec = spawn_rec(c, st, e, (spw >> 2) & 1);
+        mt_load_sc1(mt, rec, (int)ld_sc1(rec + kSpawnPos), lane);
     } else {
         mt_load(mt, st.mt + e * kMtN, st.env[e * kEnvRec + ENV_MTPOS], lane);
     }
@@ -1008,8 +1059,11 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     int cell = -1;
     bool failed = false;
     if (spst == SPAWN_READY) {
-        const uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
-        if (lane < SL) cell = (int)st.cand[(int64_t)rec[kSpawnSel + sk] * L + si];
+        const uint32_t *rec = spawn_rec(c, st, e, (spw >> 2) & 1);
+        if (lane < SL) {
+            const uint32_t sel = c.bg ? ld_sc1(rec + kSpawnSel + sk) : rec[kSpawnSel + sk];
+            cell = (int)st.cand[(int64_t)sel * L + si];
+        }
     } else {
         // The reference retries forever; a board too crowded for S disjoint spawn
         // poses would hang the wave, so give up after 2^16 permutations and flag
@@ -1077,7 +1131,9 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         int4 er;
         er.x = S; er.y = 0; er.z = c.fs - 1; er.w = mt.pos;
         *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = er;
-        if (spst != SPAWN_NONE) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spw & ~3;   // record used up
+        // record used up (background: the claim's bumped generation, buffer 0)
+        if (c.bg) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)((((uint32_t)spw >> 3) + 1u) << 3);
+        else if (spst != SPAWN_NONE) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spw & ~3;
         st.env[(int64_t)e * kEnvRec + ENV_FAIL] = failed ? 1 : 0;
         st.env[(int64_t)e * kEnvRec + ENV_VOID] = 0;
         if (failed && o.err) o.err[e] = 2;
@@ -1554,7 +1610,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     // old state (k_spawn) then fails its final compare-and-swap, or, if that landed
     // first, is overwritten here; so with bg every draw writes the word)
     const bool spw_wr = drew && (c.bg || spst != SPAWN_NONE);
-    const uint32_t spw1 = drew ? (((uint32_t)er2.x >> 2) + 1u) << 2 : (uint32_t)er2.x;
+    const uint32_t spw1 = drew ? (((uint32_t)er2.x >> 3) + 1u) << 3 : (uint32_t)er2.x;
     const int voided1 = (drew && spst != SPAWN_NONE) ? 1 : voided;   // (a record was wasted this episode)
 
     LSTAMP(45);
@@ -1580,7 +1636,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         if ((qm >> lane) & 1ull) qb[shard * c.q_cap + base + mbcnt64(qm)] = e;
     }
     // and the spawn-ahead jobs (background: with the generation they were queued at)
-    const int pent = c.bg ? (int)((uint32_t)e | ((spw1 >> 2) << (32 - kQGenBits))) : e;
+    const int pent = c.bg ? (int)((uint32_t)e | ((spw1 >> 3) << (32 - kQGenBits))) : e;
     if (pm) {
         const int base = bcast(pbase, 0);
         if ((pm >> lane) & 1ull) qb[(kQShards + shard) * c.q_cap + base + mbcnt64(pm)] = pent;
@@ -1589,7 +1645,10 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         const int base = bcast(nbase, 0);
         if ((pn >> lane) & 1ull) qb[(2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn)] = pent;
     }
-    if (env_ok && k == 0 && !bad && spw_wr) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)spw1;
+    if (env_ok && k == 0 && !bad && spw_wr) {
+        if (c.bg) atomicExch(reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN), spw1);
+        else st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)spw1;
+    }
     if (SNAKE_VOID && env_ok && k == 0 && !bad && voided1 != voided) st.env[(int64_t)e * kEnvRec + ENV_VOID] = voided1;
     LSTAMP(49);
     int rank = 1;
@@ -1652,22 +1711,33 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
 // step, so nothing else touches the env's MT state or record meanwhile.
 // The status word spw is the one the attempt started under (generation kept);
 // a background job publishes with a compare-and-swap against it (k_spawn).
-template <int MS>
+// The record goes to buffer nb. Background (k_spawn, BG): write-through stores,
+// drained, then published with a compare-and-swap against spw.
+template <int MS, bool BG = false>
 __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, const WaveMT &mt, bool ok,
-                                   const int (&q)[MS], int lane, uint32_t spw, bool cas = false)
+                                   const int (&q)[MS], int lane, uint32_t spw, int nb = 0)
 {
-    uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
-    mt_store(mt, rec, lane);
+    uint32_t *rec = spawn_rec(c, st, e, nb);
     int mine = 0;
 #pragma unroll
     for (int k = 0; k < MS; k++) mine = (lane == k) ? q[k] : mine;
-    if (ok && lane < c.S) rec[kSpawnSel + lane] = (uint32_t)mine;
-    if (lane == 0) {
-        rec[kSpawnPos] = (uint32_t)mt.pos;
-        const uint32_t w1 = (spw & ~3u) | (ok ? SPAWN_READY : SPAWN_PARTIAL);
-        uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN);
-        if (cas) atomicCAS(wp, spw, w1);
-        else *wp = w1;
+    uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN);
+    const uint32_t w1 = (spw & ~7u) | ((uint32_t)nb << 2) | (ok ? SPAWN_READY : SPAWN_PARTIAL);
+    if constexpr (BG) {
+#pragma unroll
+        for (int t = 0; t < 10; t++)
+            if (64 * t + lane < kMtN) st_sc1(rec + 64 * t + lane, mt.w[t]);
+        if (ok && lane < c.S) st_sc1(rec + kSpawnSel + lane, (uint32_t)mine);
+        if (lane == 0) st_sc1(rec + kSpawnPos, (uint32_t)mt.pos);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) atomicCAS(wp, spw, w1);
+    } else {
+        mt_store(mt, rec, lane);
+        if (ok && lane < c.S) rec[kSpawnSel + lane] = (uint32_t)mine;
+        if (lane == 0) {
+            rec[kSpawnPos] = (uint32_t)mt.pos;
+            *wp = w1;
+        }
     }
 }
 
@@ -1681,9 +1751,9 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
                          unsigned long long deadline, int lane)
 {
     WaveMT mt;
-    const int spw = load_reset_mt(st, e, mt, lane), spst = spw & 3;
+    const int spw = load_reset_mt(c, st, e, mt, lane), spst = spw & 3;
     if (spst == SPAWN_READY) return;
-    uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
+    uint32_t *rec = spawn_rec(c, st, e, 0);
     const int i0 = spst == SPAWN_INPROG ? (int)rec[kSpawnI] : -1;
     int q[MS], cell, pi = 0;
     const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, 0, q, cell, lane, i0, SLICE ? deadline : 0ull,
@@ -1694,36 +1764,45 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
         if (lane == 0) {
             rec[kSpawnPos] = (uint32_t)mt.pos;
             rec[kSpawnI] = (uint32_t)pi;
-            st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (spw & ~3) | SPAWN_INPROG;
+            st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (spw & ~7) | SPAWN_INPROG;
         }
         return;
     }
     store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)spw);
 }
 
-// Background spawn-ahead job (k_spawn) of env e, queued by the step's k_logic at
-// generation qgen. It runs beside the next step's k_logic, which may draw from
-// the env's MT state meanwhile: such a draw bumps the generation, so a job that
-// sees another generation has nothing to do, and one that read a state being
-// redrawn publishes only if its compare-and-swap still finds qgen's word (if
-// k_logic's store lands after it, that store voids the record). The record is
-// read by the next step's resets only after this kernel has ended.
+// Background spawn-ahead job (k_spawn) of env e, queued by step t's k_logic at
+// generation qgen, running beside step t's resets and step t+1 (both its rules
+// and its resets). Every writer of env e's MT state changes the generation with
+// an atomic first or last -- k_logic's draws (atomic exchange after them), an
+// auto-reset's claim (atomic add before it) -- so a job that sees another
+// generation has nothing to do, and one whose inputs were being rewritten fails
+// its final compare-and-swap (or is voided by the exchange landing after it).
+// The record goes to the buffer the status word does not point at: a reset that
+// claims the env meanwhile reads the other one, which nothing writes.
 template <int MS>
 __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_t qgen, uint8_t *lds, int lane)
 {
-    const uint32_t spw = __hip_atomic_load(reinterpret_cast<const uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (((spw >> 2) & ((1u << kQGenBits) - 1u)) != qgen || (spw & 3u) == SPAWN_READY) return;
+    uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN);
+    int v = 0;
+    if (lane == 0) v = (int)atomicAdd(wp, 0u);   // (the memory-side value)
+    const uint32_t spw = (uint32_t)__shfl(v, 0);
+    if (((spw >> 3) & ((1u << kQGenBits) - 1u)) != qgen || (spw & 3u) == SPAWN_READY) return;
+    const int buf = (spw >> 2) & 1;
     WaveMT mt;
     if ((spw & 3u) != SPAWN_NONE) {
-        const uint32_t *rec = st.spawn + (int64_t)e * kSpawnStride;
-        mt_load(mt, rec, (int)rec[kSpawnPos], lane);
+        const uint32_t *rec = spawn_rec(c, st, e, buf);
+        mt_load_sc1(mt, rec, (int)ld_sc1(rec + kSpawnPos), lane);
     } else {
         mt_load(mt, st.mt + (int64_t)e * kMtN, st.env[(int64_t)e * kEnvRec + ENV_MTPOS], lane);
     }
     int q[MS], cell;
-    const bool ok = spawn_attempt<MS, true>(c, st, mt, lds, 0, e, 0, q, cell, lane);
-    store_spawn_record<MS>(c, st, e, mt, ok, q, lane, spw, true);
+    bool ok = false;
+    for (int a = 0; a < c.bg_tries && !ok; a++) {   // (attempts until disjoint, at most bg_tries)
+        if (a > 0) wave_sync();
+        ok = spawn_attempt<MS, true>(c, st, mt, lds, 0, e, a, q, cell, lane);
+    }
+    store_spawn_record<MS, true>(c, st, e, mt, ok, q, lane, spw, buf ^ 1);
 }
 
 // Spawn-ahead right after an explicit reset (k_reset): the next episode's spawn
@@ -1742,7 +1821,7 @@ __device__ void spawn_after_reset(const KCfg &c, const snake_state &st, int e, W
     bool ok = false;
     for (int a = 0; a < kResetAheadTries && !ok; a++)
         ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, a, q, cell, lane);
-    store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)st.env[(int64_t)e * kEnvRec + ENV_SPAWN]);
+    store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)st.env[(int64_t)e * kEnvRec + ENV_SPAWN], 0);
 }
 
 // ---------------------------------------------------- step: the observation
@@ -1786,14 +1865,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     const int64_t qset = kNumQ * kQShards * c.q_cap + kQCounters;
     int *qb = st.resetq + c.qpar * qset;
     int *qc = qb + kNumQ * kQShards * c.q_cap;
-    if (c.bg && blockIdx.x == 0) {
-        // the other set's spawn counters: its k_spawn (the last step's) has ended
-        // (launch_step orders this kernel after it) and the next step that fills
-        // them (k_logic, after this kernel) has not begun
-        int *oc = st.resetq + (1 - c.qpar) * qset + kNumQ * kQShards * c.q_cap;
-        for (int q = kQShards + lane; q < kNumQ * kQShards; q += kWave) oc[q * kQSpread] = 0;
-        if (lane < kClaimShards) oc[(kQSpClaim + lane) * kQSpread] = 0;
-    }
     const int cnt = qc[lane * kQSpread], ucnt = qc[(kQShards + lane) * kQSpread],
               ncnt = qc[(2 * kQShards + lane) * kQSpread];
     const int incl = wave_scan(cnt, lane), uincl = wave_scan(ucnt, lane), nincl = wave_scan(ncnt, lane);
@@ -1827,7 +1898,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             __builtin_amdgcn_s_setprio(3);
             const int e = job_env(0, idx, incl);
             WaveMT mt;
-            const int spst = load_reset_mt(st, e, mt, lane);
+            const int spst = c.bg ? claim_reset_mt(c, st, e, mt, lane) : load_reset_mt(c, st, e, mt, lane);
             if (c.diag && lane == 0 && (spst & 3) == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
             if (idx < 128) OBSPROF(idx, lane);
             const int ps = idx < 128 ? idx : -1;
@@ -1873,11 +1944,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
 }
 
 // Background spawn-ahead (KCfg.bg): the step's spawn-ahead jobs, run by
-// spawn_slots one-wave workers on a stream of their own that the step does not
-// join -- beside the step's resets and encodes and the next step's k_logic; the
-// next step's k_autoreset waits for it (launch_step). Jobs are claimed on 16
-// claim shards like k_autoreset's; the counters are re-zeroed by the next
-// step's k_autoreset.
+// spawn_slots one-wave workers on a stream of their own that no step waits for
+// except the one two steps later, whose k_logic refills this queue set
+// (launch_step); do_spawn_bg says how they stay out of the resets' way. Jobs
+// are claimed on 16 claim shards like k_autoreset's, whose last worker
+// re-zeroes the set's spawn counters.
 template <int MS>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_spawn(const KCfg c, const snake_state st)
 {
@@ -1898,7 +1969,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         const int base = sh ? bcast(qincl, sh - 1) : 0;
         return qb[(q * kQShards + sh) * c.q_cap + j - base];
     };
-    for (int idx = blockIdx.x; idx < T;) {
+    int nx = -1;   // (a worker with no first job makes one failing claim below)
+    int idx = blockIdx.x;
+    if (idx >= T) {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(&qc[(kQSpClaim + x) * kQSpread], 1);
+        nx = bcast(v, 0);
+    }
+    for (; idx < T;) {
         const int ent = idx < U ? job_env(1, idx, uincl) : job_env(2, idx - U, nincl);
         const int e = ent & ((1 << (32 - kQGenBits)) - 1);
         const uint32_t qgen = (uint32_t)ent >> (32 - kQGenBits);
@@ -1908,7 +1986,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         if (idx < 128) OBSPROF(640 + idx, lane);
         int v = 0;
         if (lane == 0) v = atomicAdd(&qc[(kQSpClaim + x) * kQSpread], 1);
-        idx = G + x + nsh * bcast(v, 0);
+        nx = bcast(v, 0);
+        idx = G + x + nsh * nx;
+    }
+    // the shard's last claim finishes the shard; the last shard re-zeroes (as in
+    // k_autoreset, with this kernel's claim and done counters)
+    const int jobs_x = T > G + x ? (T - G - x + nsh - 1) / nsh : 0;
+    const int workers_x = (G - x + nsh - 1) / nsh;
+    if (nx == jobs_x + workers_x - 1) {
+        int d = 0;
+        if (lane == 0) d = atomicAdd(&qc[kQSpDone * kQSpread], 1);
+        if (bcast(d, 0) == nsh - 1) {
+            for (int q = kQShards + lane; q < kNumQ * kQShards; q += kWave) qc[q * kQSpread] = 0;
+            if (lane <= kClaimShards) qc[(kQSpClaim + lane) * kQSpread] = 0;   // (claims + done)
+        }
     }
 }
 
@@ -1993,14 +2084,17 @@ __global__ void __launch_bounds__(64) k_encode_multi(const KCfg c, const snake_s
 #undef SNAKE_ENC_FETCH
 }
 
-// Lean encode over c.enc_per_wave consecutive envs per wave (W % 4 == 0): the
-// next env's frames (NPW dwords per lane), current slot, crop centres and
-// reset flag are loaded into registers while this env is encoded, one memory
-// round trip per env in the shadow of the previous encode; the zero border of
-// the LDS image is written once per wave. The LDS destination of every
-// prefetched dword is the same for every env (computed once).
-template <int NPW>
-__global__ void __launch_bounds__(64) k_encode_lean(const KCfg c, const snake_state st, const snake_out o)
+// Lean encode over c.enc_per_wave consecutive envs per workgroup of T threads
+// (W % 4 == 0): the next env's frames (NPW dwords per thread), current slot,
+// crop centres and reset flag are loaded into registers while this env is
+// encoded, one memory round trip per env in the shadow of the previous encode;
+// the zero border of the LDS image is written once per workgroup. The LDS
+// destination of every prefetched dword is the same for every env (computed
+// once). T = 64 (one wave per env) for small rings; T = 256 for large ones
+// (cfg5's 40x40 x 4 frames: 1600 dwords): four waves share one LDS image, a
+// quarter of the LDS per wave, and 7 prefetched dwords per thread instead of 25.
+template <int NPW, int T>
+__global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_state st, const snake_out o)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
@@ -2011,18 +2105,22 @@ __global__ void __launch_bounds__(64) k_encode_lean(const KCfg c, const snake_st
     int *base = reinterpret_cast<int *>(lds + c.fs * c.pframe);
     uint32_t *p32 = reinterpret_cast<uint32_t *>(pf);
     const int wpr = c.W >> 2, nw = c.H * wpr, nwt = c.fs * nw, gsw = c.grid_stride >> 2, fsS = c.fs * c.S;
+    auto sync = [&]() {
+        if constexpr (T == kWave) wave_sync();
+        else __syncthreads();
+    };
     // per prefetched dword: ring word index and LDS dword index (clamped: the
-    // lanes past the end repeat the last word, same source, same destination)
+    // threads past the end repeat the last word, same source, same destination)
     int src[NPW], dst[NPW];
 #pragma unroll
     for (int u = 0; u < NPW; u++) {
-        const int x = min(lane + u * kWave, nwt - 1);
+        const int x = min(lane + u * T, nwt - 1);
         const int s = x / nw, xx = x - s * nw;
         const int r = (int)__umulhi((uint32_t)xx, c.mag_wpr), c4 = xx - r * wpr;
         src[u] = s * gsw + xx;
         dst[u] = (s * c.pframe + (r + c.vr) * c.pw + c.lp) / 4 + c4;
     }
-    zero_lean(c, pf, lane);
+    zero_lean<T>(c, pf, lane);
     const int e_begin = blockIdx.x * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
     uint32_t w[NPW];
     int pcur = 0, pctr = 0, pskip = 0;
@@ -2038,7 +2136,7 @@ __global__ void __launch_bounds__(64) k_encode_lean(const KCfg c, const snake_st
     if (e_begin < e_end) SNAKE_LEAN_FETCH(e_begin);
     for (int e = e_begin; e < e_end; e++) {
         const int cur = pcur, skip = pskip;   // (a reset env's obs is written by its reset)
-        wave_sync();                          // (the previous encode has read the LDS image)
+        sync();                               // (the previous encode has read the LDS image)
         if (!skip) {
 #pragma unroll
             for (int u = 0; u < NPW; u++) p32[dst[u]] = w[u];
@@ -2049,8 +2147,8 @@ __global__ void __launch_bounds__(64) k_encode_lean(const KCfg c, const snake_st
         }
         if (e + 1 < e_end) SNAKE_LEAN_FETCH(e + 1);   // in flight during this env's encode
         if (!skip) {
-            wave_sync();
-            encode_lean(c, pf, base, cur + 1 == c.fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lane);
+            sync();
+            encode_lean<T>(c, pf, base, cur + 1 == c.fs ? 0 : cur + 1, o.obs + (int64_t)e * c.units * 8, lane);
         }
     }
 #undef SNAKE_LEAN_FETCH
@@ -2068,7 +2166,7 @@ __global__ void __launch_bounds__(64) k_reset(const KCfg c, const snake_state st
         if (mask && !mask[e]) continue;
         STAMP(e, lane, 0);
         WaveMT mt;
-        const int spst = load_reset_mt(st, e, mt, lane);
+        const int spst = load_reset_mt(c, st, e, mt, lane);
         if (c.link_in_lds) do_reset<MS, true, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
         else do_reset<MS, false, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
         // with spawn-ahead on, the next reset's poses are drawn now, off the step
@@ -2241,13 +2339,13 @@ static int check_launch(const char *what)
 constexpr unsigned kJoinFlags = hipEventDisableTiming | hipEventDisableSystemFence;
 
 // Background spawn-ahead (KCfg.bg) per state (keyed by its env records): the
-// stream k_spawn runs on, the event recorded after the last one, the step
-// counter whose parity picks the queue set.
+// stream k_spawn runs on, the event recorded after the last one of each queue
+// set, the step counter whose parity picks the queue set.
 struct BgCtx {
     hipStream_t x = nullptr;
-    hipEvent_t done = nullptr;
+    hipEvent_t done[2] = {nullptr, nullptr};
     uint64_t steps = 0;
-    bool pending = false;
+    bool pending[2] = {false, false};
 };
 static std::mutex g_bgmu;
 static std::map<const void *, BgCtx> g_bg;
@@ -2259,11 +2357,15 @@ static BgCtx *bg_ctx(const snake_state &st, bool create)
     if (it != g_bg.end()) return &it->second;
     if (!create) return nullptr;
     BgCtx c;
-    static const char *ev_sp = getenv("SNAKE_BG_STREAM_PRIO");   // 1: the lowest stream priority
-    int least = 0, greatest = 0;
-    if (ev_sp && atoi(ev_sp)) hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (hipStreamCreateWithPriority(&c.x, hipStreamNonBlocking, least) != hipSuccess ||
-        hipEventCreateWithFlags(&c.done, kJoinFlags) != hipSuccess) {
+    static const char *ev_sp = getenv("SNAKE_BG_STREAM_PRIO");   // 1: the lowest, 2: the highest stream priority
+    int least = 0, greatest = 0, prio = 0;
+    if (ev_sp && atoi(ev_sp)) {
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+        prio = atoi(ev_sp) == 2 ? greatest : least;
+    }
+    if (hipStreamCreateWithPriority(&c.x, hipStreamNonBlocking, prio) != hipSuccess ||
+        hipEventCreateWithFlags(&c.done[0], kJoinFlags) != hipSuccess ||
+        hipEventCreateWithFlags(&c.done[1], kJoinFlags) != hipSuccess) {
         set_error("background stream / event creation failed");
         return nullptr;
     }
@@ -2274,11 +2376,12 @@ static BgCtx *bg_ctx(const snake_state &st, bool create)
 int wait_background(const snake_state &st, void *stream)
 {
     BgCtx *b = bg_ctx(st, false);
-    if (!b || !b->pending) return SNAKE_OK;
-    if (hipStreamWaitEvent((hipStream_t)stream, b->done, 0) != hipSuccess) {
-        set_error("waiting for the background spawn kernel failed");
-        return SNAKE_E_LAUNCH;
-    }
+    if (!b) return SNAKE_OK;
+    for (int p = 0; p < 2; p++)
+        if (b->pending[p] && hipStreamWaitEvent((hipStream_t)stream, b->done[p], 0) != hipSuccess) {
+            set_error("waiting for the background spawn kernel failed");
+            return SNAKE_E_LAUNCH;
+        }
     return SNAKE_OK;
 }
 
@@ -2364,9 +2467,14 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits + epw * ms * kRespawnT * 4 + epw * ms * 2;
     const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
     BgCtx *bgc = nullptr;
-    if (k.bg) {   // background spawn-ahead: this step's queue set
+    if (k.bg) {   // background spawn-ahead: this step's queue set, once the
+                  // spawn kernel of two steps ago has read it
         if (!(bgc = bg_ctx(st, true))) return SNAKE_E_LAUNCH;
         k.qpar = (int)(bgc->steps & 1);
+        if (bgc->pending[k.qpar] && hipStreamWaitEvent(sm, bgc->done[k.qpar], 0) != hipSuccess) {
+            set_error("ordering after the background spawn kernel failed");
+            return SNAKE_E_LAUNCH;
+        }
     }
     TimedLaunch t1("k_logic", sm);
     if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, k, st, actions, o);
@@ -2406,10 +2514,8 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         return SNAKE_E_LAUNCH;
     }
     if (bgc) {
-        // the resets after the last step's spawn kernel (its records), this
-        // step's spawn kernel on the background stream, not joined
-        if ((bgc->pending && hipStreamWaitEvent(sm, bgc->done, 0) != hipSuccess) ||
-            hipStreamWaitEvent(bgc->x, sc.fork, 0) != hipSuccess) {
+        // this step's spawn kernel on the background stream, not joined
+        if (hipStreamWaitEvent(bgc->x, sc.fork, 0) != hipSuccess) {
             set_error("ordering the background spawn kernel failed");
             return SNAKE_E_LAUNCH;
         }
@@ -2423,11 +2529,11 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bgc->x, ks, st);
         t4.close();
         if ((rc = check_launch("k_spawn"))) return rc;
-        if (hipEventRecord(bgc->done, bgc->x) != hipSuccess) {
+        if (hipEventRecord(bgc->done[k.qpar], bgc->x) != hipSuccess) {
             set_error("background spawn event failed");
             return SNAKE_E_LAUNCH;
         }
-        bgc->pending = true;
+        bgc->pending[k.qpar] = true;
         bgc->steps++;
     }
     static const bool resets_main = !(getenv("SNAKE_ENCODE_ON_MAIN") && atoi(getenv("SNAKE_ENCODE_ON_MAIN")));
@@ -2458,10 +2564,11 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         const int lds_enc = k.lean ? k.lds_lean_bytes : k.lds_obs_bytes;
         const dim3 ge((k.N + epw2 - 1) / epw2);
         const int n16 = k.ring_bytes >> 4;
-        const int npw = (k.fs * k.HW / 4 + kWave - 1) / kWave;   // frame dwords per lane (lean)
-        if (k.lean && npw <= 2) hipLaunchKernelGGL(k_encode_lean<2>, ge, block, lds_enc, s_enc, k, st, o);
-        else if (k.lean && npw <= 8) hipLaunchKernelGGL(k_encode_lean<8>, ge, block, lds_enc, s_enc, k, st, o);
-        else if (k.lean) hipLaunchKernelGGL(k_encode_lean<32>, ge, block, lds_enc, s_enc, k, st, o);
+        const int npw = (k.fs * k.HW / 4 + k.lean_threads - 1) / k.lean_threads;   // frame dwords per thread (lean)
+        if (k.lean && k.lean_threads == 256) hipLaunchKernelGGL((k_encode_lean<8, 256>), ge, dim3(256), lds_enc, s_enc, k, st, o);
+        else if (k.lean && npw <= 2) hipLaunchKernelGGL((k_encode_lean<2, kWave>), ge, block, lds_enc, s_enc, k, st, o);
+        else if (k.lean && npw <= 8) hipLaunchKernelGGL((k_encode_lean<8, kWave>), ge, block, lds_enc, s_enc, k, st, o);
+        else if (k.lean) hipLaunchKernelGGL((k_encode_lean<32, kWave>), ge, block, lds_enc, s_enc, k, st, o);
         else if (epw2 <= 1) hipLaunchKernelGGL(k_encode, g1, block, lds_enc, s_enc, k, st, o);
         else if (n16 <= kWave) hipLaunchKernelGGL(k_encode_multi<1>, ge, block, lds_enc, s_enc, k, st, o);
         else if (n16 <= 2 * kWave) hipLaunchKernelGGL(k_encode_multi<2>, ge, block, lds_enc, s_enc, k, st, o);

@@ -54,11 +54,12 @@ def test_plan_sizes(native):
     assert lay.spawn == 65536 * 656 * 4                        # spawn-ahead records
     assert lay.stats == 65536 * 4 * 16                         # snake_epi_stat: one 16-B record per snake
     # two sets (step parity) of three queues + counters (one per 128-B line)
-    assert lay.resetq == 2 * (3 * 64 * (4096 // 64) * 16 + 225 * 32) * 4
+    assert lay.resetq == 2 * (3 * 64 * (4096 // 64) * 16 + 226 * 32) * 4
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
     assert lay.obs_c == 32 and lay.obs == 8192 * 8 * 11 * 11 * 32
     assert lay.n_cand == 16424 and lay.jscratch == 0              # u16 draw record fits LDS
+    assert lay.spawn == 2 * 8192 * 656 * 4                        # background spawn-ahead: two records per env
     c = cfg(native, height=44, width=44, num_snakes=4)
     lay2 = native.SnakeLayout()
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay2)) == 0

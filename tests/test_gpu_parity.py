@@ -315,7 +315,7 @@ def test_reset_draws_spawn_ahead(S, kw):
     assert torch.equal(a.reset(), b.reset())
     sa, sb = a.env_rec.view(N, 8)[:, 4].cpu(), b.env_rec.view(N, 8)[:, 4].cpu()
     assert bool((sa != 0).all()) and bool((sb == 0).all())
-    assert float((sa == 2).float().mean()) > 0.9          # READY for almost every env
+    assert float(((sa & 3) == 2).float().mean()) > 0.9    # READY for almost every env (bits 0-1)
     for _ in range(2):                                     # resets from the records
         assert torch.equal(a.reset(), b.reset())
         assert torch.equal(a.grids(), b.grids())
