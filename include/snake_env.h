@@ -105,8 +105,8 @@ typedef struct {
     int64_t rew;        /* double [N][S] */
     int64_t done;       /* uint8  [N][S] */
     int64_t ep_done;    /* uint8  [N]                    1 when the step ended the episode */
-    int64_t rank;       /* int32  [N][S]                 info['rank'] where ep_done, else 0 */
-    int64_t ep_stats;   /* double [N][4][S]              info episode_* where ep_done, else 0 */
+    int64_t rank;       /* int32  [N][S]                 info['rank'] where ep_done (elsewhere not written) */
+    int64_t ep_stats;   /* double [N][4][S]              info episode_* where ep_done (elsewhere not written) */
     int64_t err;        /* int32  [N]                    1 = invalid action (reference KeyError: the
                                                          env is left unchanged, its rew/done are 0);
                                                          2 = its auto-reset gave up (below) */

@@ -42,8 +42,12 @@
 namespace snake {
 
 __device__ unsigned long long g_resets_run;   // auto-resets run (snake_timing_read "resets")
-__device__ unsigned long long g_spawn_hits;   // auto-resets that found a ready spawn-ahead record
-__device__ unsigned long long g_spawn_jobs;   // spawn-ahead attempts run
+// (diagnostic counters, spread over 64 lines by block: one address taking a
+// device-scope atomic per job serialised thousands of them on the timed steps)
+constexpr int kDiagSlots = 64, kDiagSpread = 16;
+__device__ unsigned long long g_spawn_hits[kDiagSlots * kDiagSpread];   // auto-resets that found a ready record
+__device__ unsigned long long g_spawn_jobs[kDiagSlots * kDiagSpread];   // spawn-ahead attempts run
+#define DIAG_ADD(arr) atomicAdd(&(arr)[(blockIdx.x % kDiagSlots) * kDiagSpread], 1ull)
 
 #ifdef SNAKE_STAMPS
 // Diagnostic build only: s_memtime stamps of env 0's wave at phase boundaries.
@@ -53,6 +57,10 @@ __device__ unsigned long long g_obsprof[1408];  // realtime (100 MHz) of auto-re
                                                 // then 5 words per auto-reset: 4 phase ends + spawn status
 #define OBSPROF(slot, lane)                                                          \
     do { if ((lane) == 0) g_obsprof[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define OBSMAX(slot, lane)                                                           \
+    do { if ((lane) == 0) atomicMax(&g_obsprof[slot], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
+#define OBSMIN(slot, lane)                                                           \
+    do { if ((lane) == 0) atomicMax(&g_obsprof[slot], ~(unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
 #define RPROF(ps, p, lane)                                                           \
     do { if ((ps) >= 0 && (lane) == 0) g_obsprof[768 + 5 * (ps) + (p)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define RPROF_VAL(ps, p, v, lane)                                                    \
@@ -96,6 +104,8 @@ __device__ unsigned long long g_obsprof[1408];  // realtime (100 MHz) of auto-re
 #define LSTAMP(idx) do {} while (0)
 #define RNOW() 0ull
 #define OBSPROF(slot, lane) do {} while (0)
+#define OBSMAX(slot, lane) do {} while (0)
+#define OBSMIN(slot, lane) do {} while (0)
 #define RPROF(ps, p, lane) do {} while (0)
 #define RPROF_VAL(ps, p, v, lane) do { (void)(v); } while (0)
 #endif
@@ -1210,6 +1220,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     int *qb = st.resetq + (int64_t)c.qpar * (kNumQ * kQShards * c.q_cap + kQCounters);
     int *qcnt = qb + kNumQ * kQShards * c.q_cap;
     LSTAMP(40);
+    OBSMIN(1400, lane);
     auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
     // ---- every load this step needs, issued up front
@@ -1653,11 +1664,12 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
     LSTAMP(49);
     int rank = 1;
     for (int j = 0; j < S; j++) rank += (__shfl(s0, gb + j) > s0);
-    if (isn) {           // the episode summary where it ended, zeros elsewhere
-        o.rank[(int64_t)e * S + k] = ep_end ? rank : 0;
+    if (isn && ep_end) {   // the episode summary where it ended (nothing stored elsewhere:
+                           // ~1.5 % of the envs at cfg3, 9.4 of k_logic's MB per step)
+        o.rank[(int64_t)e * S + k] = rank;
         double *es = o.ep_stats + (int64_t)e * 4 * S;
-        es[k] = ep_end ? s0 : 0.0; es[S + k] = ep_end ? (double)s1 : 0.0;
-        es[2 * S + k] = ep_end ? (double)s2 : 0.0; es[3 * S + k] = ep_end ? (double)s3 : 0.0;
+        es[k] = s0; es[S + k] = (double)s1;
+        es[2 * S + k] = (double)s2; es[3 * S + k] = (double)s3;
     }
     if (ep_end) { s0 = 0.0; s1 = s2 = s3 = 0u; }                   // _reset_epi_stats
     // a snake dead before this step keeps its statistics, record and (one frame)
@@ -1698,6 +1710,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + k] = nrec;
     }
     LSTAMP(47);
+    OBSMAX(1401, lane);
 }
 
 // ---------------------------------------------------- step: the observation
@@ -1860,6 +1873,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     // spawn job starts after it, and attempts still drawing pause at it
     const unsigned long long deadline =
         SLICE ? __builtin_amdgcn_s_memrealtime() + (unsigned long long)c.spawn_budget : 0ull;
+    OBSMIN(1406, lane);
     // the shard counts of the three queues, prefix-summed: queue index j lives
     // in the shard whose [excl, incl) holds it
     const int64_t qset = kNumQ * kQShards * c.q_cap + kQCounters;
@@ -1899,7 +1913,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             const int e = job_env(0, idx, incl);
             WaveMT mt;
             const int spst = c.bg ? claim_reset_mt(c, st, e, mt, lane) : load_reset_mt(c, st, e, mt, lane);
-            if (c.diag && lane == 0 && (spst & 3) == SPAWN_READY) atomicAdd(&g_spawn_hits, 1ull);
+            if (c.diag && lane == 0 && (spst & 3) == SPAWN_READY) DIAG_ADD(g_spawn_hits);
             if (idx < 128) OBSPROF(idx, lane);
             const int ps = idx < 128 ? idx : -1;
             if (c.link_in_lds) do_reset<MS, true, SLICE>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
@@ -1912,7 +1926,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             const int j = idx - R;
             const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
             if (!SLICE || __builtin_amdgcn_s_memrealtime() < deadline) {   // (else: queued again next step)
-                if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
+                if (c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
                 if (j < 128) OBSPROF(512 + j, lane);
                 if (c.link_in_lds) do_spawn<MS, true, SLICE>(c, st, e, lds, blockIdx.x, deadline, lane);
                 else do_spawn<MS, false, false>(c, st, e, lds, blockIdx.x, 0ull, lane);
@@ -1925,6 +1939,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         idx = G + x + nsh * nx;
         if (idx >= T) break;
     }
+    OBSMAX(1402, lane);
     // Every worker ends with exactly one failing claim, so the shard's claims
     // number its jobs + its workers, and the worker whose failing claim is the
     // shard's last finishes the shard. The last shard to finish re-zeroes the
@@ -1980,7 +1995,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         const int ent = idx < U ? job_env(1, idx, uincl) : job_env(2, idx - U, nincl);
         const int e = ent & ((1 << (32 - kQGenBits)) - 1);
         const uint32_t qgen = (uint32_t)ent >> (32 - kQGenBits);
-        if (c.diag && lane == 0) atomicAdd(&g_spawn_jobs, 1ull);
+        if (c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
         if (idx < 128) OBSPROF(512 + idx, lane);
         do_spawn_bg<MS>(c, st, e, qgen, lds, lane);
         if (idx < 128) OBSPROF(640 + idx, lane);
@@ -1989,6 +2004,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         nx = bcast(v, 0);
         idx = G + x + nsh * nx;
     }
+    OBSMAX(1405, lane);
     // the shard's last claim finishes the shard; the last shard re-zeroes (as in
     // k_autoreset, with this kernel's claim and done counters)
     const int jobs_x = T > G + x ? (T - G - x + nsh - 1) / nsh : 0;
@@ -2120,6 +2136,7 @@ __global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_sta
         src[u] = s * gsw + xx;
         dst[u] = (s * c.pframe + (r + c.vr) * c.pw + c.lp) / 4 + c4;
     }
+    OBSMIN(1404, lane);
     zero_lean<T>(c, pf, lane);
     const int e_begin = blockIdx.x * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
     uint32_t w[NPW];
@@ -2152,6 +2169,7 @@ __global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_sta
         }
     }
 #undef SNAKE_LEAN_FETCH
+    OBSMAX(1403, lane);
 }
 
 template <int MS>
@@ -2604,17 +2622,20 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
         return SNAKE_E_ARG;
     }
     const void *sym = !strcmp(kernel, "resets") ? (const void *)&snake::g_resets_run
-                    : !strcmp(kernel, "spawn_hits") ? (const void *)&snake::g_spawn_hits
-                    : !strcmp(kernel, "spawn_jobs") ? (const void *)&snake::g_spawn_jobs : nullptr;
+                    : !strcmp(kernel, "spawn_hits") ? (const void *)snake::g_spawn_hits
+                    : !strcmp(kernel, "spawn_jobs") ? (const void *)snake::g_spawn_jobs : nullptr;
     if (sym) {
-        unsigned long long n = 0, z = 0;
-        if (hipMemcpyFromSymbol(&n, sym, sizeof n) != hipSuccess ||
-            hipMemcpyToSymbol(sym, &z, sizeof z) != hipSuccess) {
+        const int n = sym == (const void *)&snake::g_resets_run ? 1 : snake::kDiagSlots * snake::kDiagSpread;
+        std::vector<unsigned long long> v(n, 0ull), z(n, 0ull);
+        if (hipMemcpyFromSymbol(v.data(), sym, n * sizeof(unsigned long long)) != hipSuccess ||
+            hipMemcpyToSymbol(sym, z.data(), n * sizeof(unsigned long long)) != hipSuccess) {
             snake::set_error("snake_timing_read: reading the reset counter failed");
             return SNAKE_E_LAUNCH;
         }
+        unsigned long long t = 0;
+        for (unsigned long long x : v) t += x;
         *total_ms = 0.0;
-        *count = (int64_t)n;
+        *count = (int64_t)t;
         return SNAKE_OK;
     }
     std::lock_guard<std::mutex> g(snake::g_tmu);

@@ -55,22 +55,26 @@ _INFO_KEYS = ('episode_done', 'rank', 'episode_scores', 'episode_steps', 'episod
 class _StepInfo(dict):
     """info of one SnakeVecEnv.step: a dict whose tensors are views of the step's
     output slab, made when first read (most callers never read most of them)."""
-    __slots__ = ('_env', '_slab')
+    __slots__ = ('_env', '_slab', '_es')
 
     def __init__(self, env, slab):
         dict.__init__(self, dict.fromkeys(_INFO_KEYS))
-        self._env, self._slab = env, slab
+        self._env, self._slab, self._es = env, slab, None
 
     def _make(self, k):
+        # rank / ep_stats are stored only where the episode ended (include/snake_env.h
+        # snake_out): zeros elsewhere are filled in here, when first read
         env, slab = self._env, self._slab
         if k == 'episode_done':
             return env._view(slab, 'ep_done')
-        if k == 'rank':
-            return env._view(slab, 'rank')
         if k == 'error':
             return env._view(slab, 'err')
-        return env._view(slab, 'ep_stats')[:, ('episode_scores', 'episode_steps', 'episode_fruits',
-                                               'episode_kills').index(k)]
+        ended = self['episode_done'].view(-1, 1)
+        if k == 'rank':
+            return env._view(slab, 'rank').masked_fill(~ended, 0)
+        if self._es is None:
+            self._es = env._view(slab, 'ep_stats').masked_fill(~ended.view(-1, 1, 1), 0.0)
+        return self._es[:, ('episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills').index(k)]
 
     def __getitem__(self, k):
         v = dict.__getitem__(self, k)

@@ -25,6 +25,22 @@ CFGS = {'cfg3': (65536, 4, dict(height=20, width=20, snake_length=3, vision_rang
         'cfg5': (8192, 8, dict(height=40, width=40, snake_length=3, vision_range=5, frame_stack=4))}
 
 
+def spans(r):
+    """kernel spans, us from k_logic's first wave: r = obsprof words 1400.. (starts
+    stored complemented by the max-atomics, ends plain; 0 = not recorded)"""
+    M = (1 << 64) - 1
+    t0 = M - r[0] if r[0] else None
+    out = {}
+    for n, i, inv in (('logic_end', 1, 0), ('autoreset_start', 6, 1), ('autoreset_end', 2, 0),
+                      ('encode_start', 4, 1), ('encode_end', 3, 0), ('spawn_end', 5, 0)):
+        v = r[i]
+        if not v or t0 is None:
+            out[n] = None
+            continue
+        out[n] = round(((M - v) if inv else v) - t0) / 100.0
+    return out
+
+
 def main():
     import argparse
     ap = argparse.ArgumentParser()
@@ -79,6 +95,10 @@ def main():
             'spawn_dur_us': pct((se[sok] - ss[sok]) / 100.0) if sok.any() else None,
             # per reset: status at start (0 none, 1 partial, 2 ready, 3 in progress) and the
             # phase durations: poses, paint, fruits, grid/key stores, encode
+            # kernel spans (us from k_logic block 0's start): k_logic end, k_autoreset end,
+            # lean encode start (block 0) / end, k_spawn end
+            'spans_us': spans([int(x) for x in buf[1400:1408]]),
+            'spans_raw': [int(x) for x in buf[1400:1408]],
             'reset_phases_us': [[int(p[4]) & 3] + [round(float(x), 1) for x in np.diff(
                 np.array([r, p[0], p[1], p[2], p[3], en], dtype=np.int64)) / 100.0]
                 for r, p, en in zip(rs, ph, re_)][:12],
