@@ -505,13 +505,16 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         for (int64_t u = 0; exact && u < k->units; u++) {
             const int64_t q = ((uint64_t)u * k->mag_ups) >> 32, r0 = u - q * k->ups;
             const int64_t i = ((uint64_t)r0 * k->mag_rowl) >> 32, r1 = r0 - i * k->rowl;
-            const int64_t j = ((uint64_t)r1 * k->mag_fs) >> 32;
+            const int64_t j = k->fs == 1 ? r1 : ((uint64_t)r1 * k->mag_fs) >> 32;   // (snake_kernels.hip fdiv)
             exact = q == u / k->ups && i == r0 / k->rowl && j == r1 / k->fs;
         }
         if (k->W % 4 == 0)
             for (int64_t x = 0; exact && x < (int64_t)k->HW / 4; x++)
-                exact = (int64_t)(((uint64_t)x * k->mag_wpr) >> 32) == x / (k->W / 4);
-        k->lean = want && exact ? 1 : 0;
+                exact = (k->W / 4 == 1 ? x : (int64_t)(((uint64_t)x * k->mag_wpr) >> 32)) == x / (k->W / 4);
+        // default: only the four-wave form (rings over 512 dwords: cfg5 k_encode 91 ->
+        // 66 us); one wave per env measured slower beside the reset workers (cfg3
+        // step 0.1216 vs 0.1032 ms, cfg2 0.0639 vs 0.0621; SNAKE_LEAN=1 forces it)
+        k->lean = exact && (ev_lean ? want : (want && k->lean_threads == 256)) ? 1 : 0;
     }
     // envs per encode wave (k_encode_multi: the next env's ring prefetched into
     // registers, at most 8 16-byte chunks per lane); SNAKE_ENC_PER_WAVE overrides
@@ -521,7 +524,10 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
 #define SNAKE_EPW_DEFAULT 2
 #endif
         // (measured: 2 with the lean encode at cfg3/cfg2; one env per wave otherwise)
-        int epw = ev_epw ? atoi(ev_epw) : (k->lean ? (k->lean_threads == kWave ? SNAKE_EPW_DEFAULT : 2) : 1);
+        // (k_encode_multi, two envs per wave, for large batches: cfg3 step 0.1033 ->
+        // 0.0998 ms; cfg2's 4096 envs keep one per wave, 0.0622 vs 0.0625)
+        int epw = ev_epw ? atoi(ev_epw)
+                         : (k->lean ? (k->lean_threads == kWave ? SNAKE_EPW_DEFAULT : 2) : (N >= 16384 ? 2 : 1));
         if (k->ring_bytes > 8 * 1024 && !k->lean) epw = 1;
         k->enc_per_wave = std::max(1, std::min(epw, 64));
     }

@@ -142,6 +142,9 @@ __device__ __forceinline__ uint32_t link_get(const gu32 *p)
 __device__ __forceinline__ int dir_dr(int d) { return d == 0 ? -1 : (d == 2 ? 1 : 0); }
 __device__ __forceinline__ int dir_dc(int d) { return d == 1 ? 1 : (d == 3 ? -1 : 0); }
 __device__ __forceinline__ int div10(int v) { return (v * 205) >> 11; }  // exact for 0 <= v < 1029
+// x / d by the multiply-high reciprocal m = ceil(2^32 / d) (snake_capi.cpp);
+// d == 1 has no 32-bit reciprocal (m wraps to 0)
+__device__ __forceinline__ int fdiv(uint32_t x, uint32_t m, int d) { return d == 1 ? (int)x : (int)__umulhi(x, m); }
 
 // LDS hand-off between lanes of the single wave of a workgroup: LDS executes a
 // wave's instructions in order, so only the compiler must not move memory
@@ -772,7 +775,7 @@ __device__ void encode_lean(const KCfg &c, const uint8_t *pf, const int *base, i
         const int r0 = (int)u - kk * c.ups;
         int ii = (int)__umulhi((uint32_t)r0, c.mag_rowl);
         const int r1 = r0 - ii * c.rowl;
-        int jj = (int)__umulhi((uint32_t)r1, c.mag_fs);
+        int jj = fdiv((uint32_t)r1, c.mag_fs, c.fs);
         int ff = r1 - jj * c.fs;
         uint32_t w[4];
 #pragma unroll
@@ -814,7 +817,7 @@ __device__ void stage_lean(const KCfg &c, const snake_state &st, int64_t e, uint
         uint32_t *p32 = reinterpret_cast<uint32_t *>(pf);
         for (int s = 0; s < c.fs; s++)
             for (int x = lane; x < nw; x += kWave) {
-                const int r = (int)__umulhi((uint32_t)x, c.mag_wpr), c4 = x - r * wpr;
+                const int r = fdiv((uint32_t)x, c.mag_wpr, wpr), c4 = x - r * wpr;
                 p32[(s * c.pframe + (r + tp) * c.pw + c.lp) / 4 + c4] = r32[s * (c.grid_stride >> 2) + x];
             }
     } else {
@@ -1262,7 +1265,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const int q = min(q0 + u * kWave + lane, nq - 1);
-                const int gg = (int)__umulhi((uint32_t)q, c.mag_n16), off = q - gg * n16;
+                const int gg = fdiv((uint32_t)q, c.mag_n16, n16), off = q - gg * n16;
                 const int cg = ONE ? 0 : __shfl(cur, gg * G);
                 const int64_t ee = min(e0 + gg, c.N - 1);
                 v[u] = src[(ee * c.ring_bytes + (int64_t)cg * stride) / 16 + off];
@@ -1685,7 +1688,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         uint4 *dst = reinterpret_cast<uint4 *>(st.grid);
         const uint4 *s4 = reinterpret_cast<const uint4 *>(lds);
         for (int q0 = 0; q0 < E * n16; q0 += kWave) {
-            const int q = q0 + lane, gg = min((int)__umulhi((uint32_t)q, c.mag_n16), E - 1);
+            const int q = q0 + lane, gg = min(fdiv((uint32_t)q, c.mag_n16, n16), E - 1);
             const int off = q - gg * n16;
             const int ng = __shfl(ncur, gg * G);
             const int bg = __shfl((int)bad, gg * G);
@@ -2132,7 +2135,7 @@ __global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_sta
     for (int u = 0; u < NPW; u++) {
         const int x = min(lane + u * T, nwt - 1);
         const int s = x / nw, xx = x - s * nw;
-        const int r = (int)__umulhi((uint32_t)xx, c.mag_wpr), c4 = xx - r * wpr;
+        const int r = fdiv((uint32_t)xx, c.mag_wpr, wpr), c4 = xx - r * wpr;
         src[u] = s * gsw + xx;
         dst[u] = (s * c.pframe + (r + c.vr) * c.pw + c.lp) / 4 + c4;
     }
