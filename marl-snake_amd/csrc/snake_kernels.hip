@@ -112,6 +112,29 @@ __device__ unsigned long long g_obsprof[1408];  // realtime (100 MHz) of auto-re
 
 enum { C_EMPTY = 0, C_WALL = 1, C_FRUIT = 2, C_HEAD = 3, C_BODY = 4, C_TAIL = 5 };
 
+// The step and reset kernels take their arguments as one struct and read them
+// through kargs(): a pointer to the kernarg segment that the compiler cannot see
+// through (an empty asm), taken afresh at each phase or job. Every field is then
+// an s_load next to its use (the segment is constant, scalar-cached) instead of
+// a value held in an SGPR from the kernel's entry to its end: with the whole
+// KCfg, snake_state and snake_out live across a worker's job loop the compiler
+// spilled 230-300 SGPRs into VGPR lanes, 1 100-1 700 v_readlane reloads and
+// 128 VGPRs (profiles/r03_isa_counts.jsonl).
+struct KArgs {
+    KCfg c;
+    snake_state st;
+    snake_out o;
+    const void *aux;   // k_logic: the actions; k_reset: the env mask
+};
+
+__device__ __forceinline__ const KArgs &kargs()
+{
+    typedef const __attribute__((address_space(4))) KArgs KA4;
+    KA4 *p = (KA4 *)__builtin_amdgcn_kernarg_segment_ptr();   // (the first explicit argument is at offset 0)
+    __asm__ volatile("" : "+s"(p));
+    return *(const KArgs *)p;
+}
+
 // global-memory views (explicit address space: flat accesses would also count
 // against lgkmcnt and stall every LDS/cross-lane wait behind them)
 typedef __attribute__((address_space(3))) uint16_t lu16;
@@ -1199,10 +1222,13 @@ __device__ __forceinline__ void stage_to_lds(uint8_t *dst, const uint8_t *src, i
 // auto-reset. The wave-wide parts (dying-body erase, fruit respawn) loop over the
 // block's envs that need them.
 template <int MS>
-__global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c, const snake_state st,
-                                                              const int8_t *__restrict__ actions,
-                                                              const snake_out o)
+__global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
 {
+    const KArgs &A = kargs();
+    const KCfg &c = A.c;
+    const snake_state &st = A.st;
+    const snake_out &o = A.o;
+    const int8_t *__restrict__ actions = (const int8_t *)A.aux;
     constexpr int G = MS, E = kWave / MS;
     constexpr uint32_t gmask = (1u << G) - 1u;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1259,20 +1285,24 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KCfg c
         const uint4 *src = reinterpret_cast<const uint4 *>(st.grid);
         uint4 *d4 = reinterpret_cast<uint4 *>(lds);
         const int nq = E * n16;
+        // (vector values, not arrays: the arrays were demoted to scratch)
+        typedef uint32_t v32u __attribute__((ext_vector_type(32)));
+        typedef int v8i __attribute__((ext_vector_type(8)));
         for (int q0 = 0; q0 < nq; q0 += 8 * kWave) {   // uniform trip count (the __shfl)
-            uint4 v[8];
-            int qq[8];
+            v32u v;
+            v8i qq;
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const int q = min(q0 + u * kWave + lane, nq - 1);
                 const int gg = fdiv((uint32_t)q, c.mag_n16, n16), off = q - gg * n16;
                 const int cg = ONE ? 0 : __shfl(cur, gg * G);
                 const int64_t ee = min(e0 + gg, c.N - 1);
-                v[u] = src[(ee * c.ring_bytes + (int64_t)cg * stride) / 16 + off];
+                const uint4 x = src[(ee * c.ring_bytes + (int64_t)cg * stride) / 16 + off];
+                v[4 * u] = x.x; v[4 * u + 1] = x.y; v[4 * u + 2] = x.z; v[4 * u + 3] = x.w;
                 qq[u] = q;
             }
 #pragma unroll
-            for (int u = 0; u < 8; u++) d4[qq[u]] = v[u];
+            for (int u = 0; u < 8; u++) d4[qq[u]] = make_uint4(v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
         }
     };
     if (fs == 1) stage(std::true_type{});
@@ -1866,12 +1896,16 @@ __device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st,
 }
 
 // RO: resets only (every-step mode, background spawn-ahead): no spawn-job path,
-// fewer registers.
-template <int MS, bool SLICE, bool RO = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KCfg c, const snake_state st, const snake_out o)
+// fewer registers. JL: the draw record in LDS (KCfg.link_in_lds), else the
+// global link tables; one path per instantiation.
+template <int MS, bool SLICE, bool RO, bool JL>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KArgs)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
+    const KArgs &A = kargs();
+    const KCfg &c = A.c;
+    const snake_state &st = A.st;
     // the spawn-ahead time slice of this step (KCfg.spawn_budget, SLICE only): no
     // spawn job starts after it, and attempts still drawing pause at it
     const unsigned long long deadline =
@@ -1911,28 +1945,33 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     // shard x = w % kClaimShards, whose n-th claim is job G + x + kClaimShards * n.
     int idx = blockIdx.x, nx = 0;
     for (;;) {
+        // (the arguments afresh for each job: nothing of them stays live across
+        // jobs; so is the lane index, or every lane mask derived from it -- the
+        // MT word bounds, the scan steps -- would be held, spilled, for the whole
+        // kernel instead of recomputed by one compare)
+        const KArgs &J = kargs();
+        int lane = threadIdx.x;
+        __asm__ volatile("" : "+v"(lane));
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
             const int e = job_env(0, idx, incl);
             WaveMT mt;
-            const int spst = c.bg ? claim_reset_mt(c, st, e, mt, lane) : load_reset_mt(c, st, e, mt, lane);
-            if (c.diag && lane == 0 && (spst & 3) == SPAWN_READY) DIAG_ADD(g_spawn_hits);
+            const int spst = J.c.bg ? claim_reset_mt(J.c, J.st, e, mt, lane) : load_reset_mt(J.c, J.st, e, mt, lane);
+            if (J.c.diag && lane == 0 && (spst & 3) == SPAWN_READY) DIAG_ADD(g_spawn_hits);
             if (idx < 128) OBSPROF(idx, lane);
             const int ps = idx < 128 ? idx : -1;
-            if (c.link_in_lds) do_reset<MS, true, SLICE>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
-            else do_reset<MS, false, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane, ps);
+            do_reset<MS, JL, SLICE && JL>(J.c, J.st, J.o, e, mt, lds, blockIdx.x, spst, lane, ps);
             if (idx < 128) OBSPROF(128 + idx, lane);
         } else if (!RO && idx < R + P) {
-            if (c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
-            else if (c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
+            if (J.c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
+            else if (J.c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(2);
             const int j = idx - R;
             const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
             if (!SLICE || __builtin_amdgcn_s_memrealtime() < deadline) {   // (else: queued again next step)
-                if (c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
+                if (J.c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
                 if (j < 128) OBSPROF(512 + j, lane);
-                if (c.link_in_lds) do_spawn<MS, true, SLICE>(c, st, e, lds, blockIdx.x, deadline, lane);
-                else do_spawn<MS, false, false>(c, st, e, lds, blockIdx.x, 0ull, lane);
+                do_spawn<MS, JL, SLICE && JL>(J.c, J.st, e, lds, blockIdx.x, JL ? deadline : 0ull, lane);
                 if (j < 128) OBSPROF(640 + j, lane);
             }
         }
@@ -1968,8 +2007,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
 // are claimed on 16 claim shards like k_autoreset's, whose last worker
 // re-zeroes the set's spawn counters.
 template <int MS>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_spawn(const KCfg c, const snake_state st)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_spawn(const KArgs)
 {
+    const KArgs &A = kargs();
+    const KCfg &c = A.c;
+    const snake_state &st = A.st;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
     if (c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
@@ -2000,7 +2042,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         const uint32_t qgen = (uint32_t)ent >> (32 - kQGenBits);
         if (c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
         if (idx < 128) OBSPROF(512 + idx, lane);
-        do_spawn_bg<MS>(c, st, e, qgen, lds, lane);
+        const KArgs &J = kargs();
+        do_spawn_bg<MS>(J.c, J.st, e, qgen, lds, lane);
         if (idx < 128) OBSPROF(640 + idx, lane);
         int v = 0;
         if (lane == 0) v = atomicAdd(&qc[(kQSpClaim + x) * kQSpread], 1);
@@ -2175,26 +2218,24 @@ __global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_sta
     OBSMAX(1403, lane);
 }
 
-template <int MS>
-__global__ void __launch_bounds__(64) k_reset(const KCfg c, const snake_state st,
-                                              const uint8_t *__restrict__ mask, const snake_out o)
+template <int MS, bool JL>
+__global__ void __launch_bounds__(64) k_reset(const KArgs)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
-    // one env per block with the link table in LDS, else reset_slots workers
-    // striding over the envs, each with its own global link table
-    for (int e = blockIdx.x; e < c.N; e += gridDim.x) {
+    // one env per block with the link table in LDS (JL), else reset_slots
+    // workers striding over the envs, each with its own global link table
+    for (int e = blockIdx.x; e < kargs().c.N; e += gridDim.x) {
+        const KArgs &J = kargs();
+        const uint8_t *mask = (const uint8_t *)J.aux;
         if (mask && !mask[e]) continue;
         STAMP(e, lane, 0);
         WaveMT mt;
-        const int spst = load_reset_mt(c, st, e, mt, lane);
-        if (c.link_in_lds) do_reset<MS, true, true>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
-        else do_reset<MS, false, false>(c, st, o, e, mt, lds, blockIdx.x, spst, lane);
+        const int spst = load_reset_mt(J.c, J.st, e, mt, lane);
+        do_reset<MS, JL, JL>(J.c, J.st, J.o, e, mt, lds, blockIdx.x, spst, lane);
         // with spawn-ahead on, the next reset's poses are drawn now, off the step
-        if (c.spawn_thr >= 0) {
-            if (c.link_in_lds) spawn_after_reset<MS, true>(c, st, e, mt, lds, blockIdx.x, lane);
-            else spawn_after_reset<MS, false>(c, st, e, mt, lds, blockIdx.x, lane);
-        }
+        const KArgs &J2 = kargs();
+        if (J2.c.spawn_thr >= 0) spawn_after_reset<MS, JL>(J2.c, J2.st, e, mt, lds, blockIdx.x, lane);
     }
 }
 
@@ -2441,9 +2482,17 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
     if (int rc = wait_background(st, stream)) return rc;
     TimedLaunch tl("k_reset", (hipStream_t)stream);
-    if (k.S <= 4) hipLaunchKernelGGL(k_reset<4>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
-    else if (k.S <= 8) hipLaunchKernelGGL(k_reset<8>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
-    else hipLaunchKernelGGL(k_reset<16>, grid, block, k.lds_bytes, (hipStream_t)stream, k, st, mask, o);
+    const KArgs a{k, st, o, mask};
+    const hipStream_t s = (hipStream_t)stream;
+    if (k.link_in_lds) {
+        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, true>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, true>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_reset<16, true>), grid, block, k.lds_bytes, s, a);
+    } else {
+        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, false>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, false>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_reset<16, false>), grid, block, k.lds_bytes, s, a);
+    }
     tl.close();
     return check_launch("k_reset");
 }
@@ -2476,6 +2525,22 @@ static int side_ctx(hipStream_t main, int dev, SideCtx *out)
     return SNAKE_OK;
 }
 
+// k_autoreset<MS(S), SLICE, RO, JL(k.link_in_lds)>
+template <bool SLICE, bool RO>
+static void launch_autoreset(const KCfg &k, const KArgs &a, dim3 grid, hipStream_t s)
+{
+    const dim3 block(kWave);
+    if (k.link_in_lds) {
+        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, SLICE, RO, true>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, SLICE, RO, true>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_autoreset<16, SLICE, RO, true>), grid, block, k.lds_bytes, s, a);
+    } else if constexpr (!SLICE) {   // (sliced attempts exist only with the LDS record)
+        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false, RO, false>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false, RO, false>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_autoreset<16, false, RO, false>), grid, block, k.lds_bytes, s, a);
+    }
+}
+
 int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, const snake_out &o,
                 void *stream)
 {
@@ -2498,18 +2563,17 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         }
     }
     TimedLaunch t1("k_logic", sm);
-    if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, k, st, actions, o);
-    else if (ms == 8) hipLaunchKernelGGL(k_logic<8>, gl, block, lds_logic, sm, k, st, actions, o);
-    else hipLaunchKernelGGL(k_logic<16>, gl, block, lds_logic, sm, k, st, actions, o);
+    const KArgs la{k, st, o, actions};
+    if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, la);
+    else if (ms == 8) hipLaunchKernelGGL(k_logic<8>, gl, block, lds_logic, sm, la);
+    else hipLaunchKernelGGL(k_logic<16>, gl, block, lds_logic, sm, la);
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;
     if (k.autoreset == 2) {   // every env resets (the resets write the obs), then the
                               // encodes of the envs rejected for an invalid action
         TimedLaunch t2("k_autoreset", sm);
-        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false, true>), gr, block, k.lds_bytes, sm, k, st, o);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false, true>), gr, block, k.lds_bytes, sm, k, st, o);
-        else hipLaunchKernelGGL((k_autoreset<16, false, true>), gr, block, k.lds_bytes, sm, k, st, o);
+        launch_autoreset<false, true>(k, KArgs{k, st, o, nullptr}, gr, sm);
         t2.close();
         if ((rc = check_launch("k_autoreset"))) return rc;
         TimedLaunch t3("k_encode", sm);
@@ -2545,9 +2609,10 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         const int lds_sp = (int)(((int64_t)2 * (k.n_cand + kWave) + 15) / 16 * 16);
         const dim3 gs(k.spawn_slots);
         TimedLaunch t4("k_spawn", bgc->x);
-        if (k.S <= 4) hipLaunchKernelGGL(k_spawn<4>, gs, block, lds_sp, bgc->x, ks, st);
-        else if (k.S <= 8) hipLaunchKernelGGL(k_spawn<8>, gs, block, lds_sp, bgc->x, ks, st);
-        else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bgc->x, ks, st);
+        const KArgs sa{ks, st, o, nullptr};
+        if (k.S <= 4) hipLaunchKernelGGL(k_spawn<4>, gs, block, lds_sp, bgc->x, sa);
+        else if (k.S <= 8) hipLaunchKernelGGL(k_spawn<8>, gs, block, lds_sp, bgc->x, sa);
+        else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bgc->x, sa);
         t4.close();
         if ((rc = check_launch("k_spawn"))) return rc;
         if (hipEventRecord(bgc->done[k.qpar], bgc->x) != hipSuccess) {
@@ -2563,19 +2628,10 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         TimedLaunch t2("k_autoreset", s_res);
         // (the sliced form only where a time slice is set: its pause bookkeeping
         // costs registers in every job)
-        if (k.spawn_budget) {
-            if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true>), gr, block, k.lds_bytes, s_res, k, st, o);
-            else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true>), gr, block, k.lds_bytes, s_res, k, st, o);
-            else hipLaunchKernelGGL((k_autoreset<16, true>), gr, block, k.lds_bytes, s_res, k, st, o);
-        } else if (k.bg) {
-            if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false, true>), gr, block, k.lds_bytes, s_res, k, st, o);
-            else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false, true>), gr, block, k.lds_bytes, s_res, k, st, o);
-            else hipLaunchKernelGGL((k_autoreset<16, false, true>), gr, block, k.lds_bytes, s_res, k, st, o);
-        } else {
-            if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false>), gr, block, k.lds_bytes, s_res, k, st, o);
-            else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false>), gr, block, k.lds_bytes, s_res, k, st, o);
-            else hipLaunchKernelGGL((k_autoreset<16, false>), gr, block, k.lds_bytes, s_res, k, st, o);
-        }
+        const KArgs a{k, st, o, nullptr};
+        if (k.spawn_budget && k.link_in_lds) launch_autoreset<true, false>(k, a, gr, s_res);
+        else if (k.bg) launch_autoreset<false, true>(k, a, gr, s_res);
+        else launch_autoreset<false, false>(k, a, gr, s_res);
         t2.close();
         return check_launch("k_autoreset");
     };

@@ -14,7 +14,7 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, 'marl-snake_amd', 'csrc', 'snake_kernels.hip')
+SRC = os.environ.get("SRC", os.path.join(ROOT, "marl-snake_amd", "csrc", "snake_kernels.hip"))
 FLAGS = ['-O3', '-std=c++17', '-ffp-contract=off', '--offload-arch=gfx950', '-mllvm',
          '-amdgpu-atomic-optimizer-strategy=None', '--cuda-device-only']
 
