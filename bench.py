@@ -20,16 +20,20 @@ A step = one SnakeVecEnv.step() over the GPU's whole batch. The timed region is
 exactly K steps between barrier + synchronize on both sides; value = all envs of
 all ranks x K / the slowest rank's time.
 
-A step is three kernels (include/snake_env.h snake_step): k_logic (rules, all
-envs), then k_autoreset (the step's auto-resets, then the spawn-ahead attempts:
-next resets' permutations drawn early) concurrently with k_encode (the
-observations of every other env, on the library's side stream).
+A step is two launches at cfg2/cfg3 (include/snake_env.h snake_step): k_logic
+(rules, all envs), then k_post, whose first blocks are the reset workers (the
+step's auto-resets, then the spawn-ahead attempts: next resets' permutations
+drawn early) and the rest the observations of every other env. Where k_post
+does not apply (background spawn-ahead, cfg5) the workers (k_autoreset) and the
+encodes (k_encode) are two launches forked onto two streams.
 
 The JSON line also carries:
-  roofline     -- k_encode, the kernel that moves the bulk of SURVEY.md 8(d)'s
-                  bytes: per launch (N - resets) x (S*h*w*8*fs obs write + fs*H*W
-                  frame reads) / its average duration, timed by the library's HIP
-                  timing events on k_encode's own stream during the timed region
+  roofline     -- the kernel that moves the bulk of SURVEY.md 8(d)'s bytes:
+                  k_post (or k_encode), per launch (N - resets) x (S*h*w*8*fs obs
+                  write + fs*H*W frame reads) [+ for k_post, per reset 2 MT keys +
+                  fs*H*W + S*h*w*8*fs, per spawn-ahead attempt 2 MT keys + the
+                  pose indices] / its average duration, timed by the library's HIP
+                  timing events on its own stream during the timed region
                   (snake_timing_enable; every --timing-stride-th step, default 32),
                   against the 8 TB/s HBM peak; `traffic` is null (the HBM bytes of
                   a launch come from rocprofv3 PMC passes, committed under
@@ -87,6 +91,22 @@ def encode_bytes(S, h, w, fs, H, W):
     """k_encode per encoded env: the stacked-frame observation written + the fs
     grid frames read."""
     return S * h * w * 8 * fs + fs * H * W
+
+
+MT_KEY_BYTES = 624 * 4
+
+
+def reset_bytes(S, h, w, fs, H, W):
+    """One auto-reset (do_reset from a ready spawn-ahead record): the MT key read
+    from the record and stored back, the fs fresh frames and the first
+    observation written."""
+    return 2 * MT_KEY_BYTES + fs * H * W + S * h * w * 8 * fs
+
+
+def spawn_bytes(S):
+    """One spawn-ahead attempt: the env's MT key read, the record (key, position,
+    S pose indices) written."""
+    return 2 * MT_KEY_BYTES + 4 * (1 + S)
 
 
 PRESETS = {   # BASELINE.json configs (per GPU)
@@ -228,7 +248,7 @@ def main():
     torch.cuda.synchronize(device)
 
     L = _native.lib()
-    for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_spawn', 'resets', 'spawn_hits', 'spawn_jobs'):
+    for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_post', 'k_spawn', 'resets', 'spawn_hits', 'spawn_jobs'):
         _native.timing_read(k, L)                      # drop anything from the warmup
     stride = args.timing_stride
     if distributed:
@@ -252,7 +272,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kern = {}
-    for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_spawn'):
+    for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_post', 'k_spawn'):
         ms, n = _native.timing_read(k, L)
         kern[k] = ms / max(n, 1)
     resets = _native.timing_read('resets', L)[1]
@@ -268,8 +288,18 @@ def main():
     B = algorithmic_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
     Be = encode_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
     encoded_per_launch = (hi - lo) - resets / args.steps
-    enc_ms = kern['k_encode']
-    achieved = Be * encoded_per_launch / (enc_ms * 1e-3) / 1e9 if enc_ms > 0 else float('nan')
+    if kern['k_post'] > 0:
+        # the shared phase as one launch (k_post: reset workers + encodes): its
+        # bytes are the encodes', the resets' and the spawn-ahead attempts'
+        rk, rk_ms = 'k_post', kern['k_post']
+        jobs_per_step = sp_jobs / n_timed if n_timed else 0.0
+        launch_bytes = (Be * encoded_per_launch
+                        + reset_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
+                        * resets / args.steps + spawn_bytes(S) * jobs_per_step)
+    else:
+        rk, rk_ms = 'k_encode', kern['k_encode']
+        launch_bytes = Be * encoded_per_launch
+    achieved = launch_bytes / (rk_ms * 1e-3) / 1e9 if rk_ms > 0 else float('nan')
     value = n_total * args.steps / elapsed
     step_gbs = B * (hi - lo) / (elapsed / args.steps) / 1e9
     preset = PRESETS[args.config]
@@ -297,8 +327,8 @@ def main():
                    'snake_length': 3, 'parallelism': f'env-shard x{world}'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                     'traffic': None, 'kernel': 'k_encode', 'kernel_ms': round(enc_ms, 4),
-                     'algorithmic_bytes_per_launch': round(Be * encoded_per_launch),
+                     'traffic': None, 'kernel': rk, 'kernel_ms': round(rk_ms, 4),
+                     'algorithmic_bytes_per_launch': round(launch_bytes),
                      'bytes_per_encoded_env': Be},
         'step_roofline': {'achieved': round(step_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                           'frac': round(step_gbs / HBM_PEAK_GBS, 4), 'bytes_per_env_step': B},

@@ -180,9 +180,12 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
 /* SnakeEnv.step(actions) (snake_env.py:301-414) for all envs at once; actions is
  * int8 [N][S]. With cfg->autoreset an env whose dones are all True is reset in
  * the same call and its out->obs holds the reset observation. Launches: k_logic
- * (the game rules of every env, queueing the auto-resets), then k_autoreset on
- * `stream` concurrently with k_encode (every other env's observation) on a side
- * stream the library keeps per caller stream; joined before the call returns.
+ * (the game rules of every env, queueing the auto-resets), then k_post on
+ * `stream`, whose first blocks are the reset workers and the rest the encodes of
+ * every other env's observation. With background spawn-ahead or a spawn time
+ * slice the workers (k_autoreset) run on `stream` concurrently with k_encode on a
+ * side stream the library keeps per caller stream, joined before the call
+ * returns.
  *
  * Spawn-ahead: a reset's spawn poses depend only on the env's MT19937 state, which
  * changes only at fruit respawns and resets. With autoreset, k_logic also queues
@@ -220,7 +223,7 @@ int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_en
 /* Profiling aid. While enabled, every kernel launch of snake_step / snake_reset
  * is bracketed by timing events on its own stream. snake_timing_read returns the
  * summed device time (ms) and the launch count of one kernel ("k_logic",
- * "k_autoreset", "k_encode", "k_reset") since its last read, and the number of
+ * "k_post", "k_autoreset", "k_encode", "k_spawn", "k_reset") since its last read, and the number of
  * auto-resets run (kernel "resets": count only); it waits for the events.
  * "spawn_hits" / "spawn_jobs" count (while enabled) the auto-resets that started
  * from a ready spawn-ahead record and the spawn-ahead attempts run. */

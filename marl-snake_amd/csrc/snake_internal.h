@@ -85,6 +85,7 @@ struct KCfg {
     int draws_stride;           // u16 entries per env in st.spawn_draws (0: attempts are not sliced)
     int enc_per_wave;           // envs per k_encode wave (1: k_encode, else k_encode_multi with prefetch)
     int bg;                     // 1: spawn-ahead jobs in the background kernel k_spawn (not k_autoreset)
+    int fused;                  // 1: reset workers and encodes in one launch (k_post), no side stream
     int qpar;                   // queue set of this step (0 unless bg)
     int spawn_slots;            // k_spawn workers
     int bg_tries;               // k_spawn: permutation attempts per job (until disjoint)

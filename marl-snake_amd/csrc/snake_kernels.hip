@@ -1898,8 +1898,9 @@ __device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st,
 // RO: resets only (every-step mode, background spawn-ahead): no spawn-job path,
 // fewer registers. JL: the draw record in LDS (KCfg.link_in_lds), else the
 // global link tables; one path per instantiation.
+// wid = this worker (0 .. G-1): k_autoreset's block, or a block of k_post.
 template <int MS, bool SLICE, bool RO, bool JL>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KArgs)
+__device__ __forceinline__ void autoreset_worker(const int wid, const int G)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
@@ -1921,15 +1922,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     const int incl = wave_scan(cnt, lane), uincl = wave_scan(ucnt, lane), nincl = wave_scan(ncnt, lane);
     const int R = bcast(incl, kWave - 1), U = bcast(uincl, kWave - 1);
     // claim shards: min(G, kClaimShards), so that every shard has a worker
-    const int G = (int)gridDim.x, nsh = min(G, kClaimShards);
-    const int x = G >= kClaimShards ? (int)(blockIdx.x & (kClaimShards - 1)) : (int)blockIdx.x % nsh;
+    const int nsh = min(G, kClaimShards);
+    const int x = G >= kClaimShards ? (wid & (kClaimShards - 1)) : wid % nsh;
     // spawn_cap: the other (2-live-snake) jobs only as far as the first round
     // of workers reaches; their envs are queued again next step
     int Nn = bcast(nincl, kWave - 1);
     if (c.spawn_cap) Nn = min(Nn, max(G - R - U, 0));
     const int P = (RO || c.bg) ? 0 : U + Nn;   // (background: the spawn jobs are k_spawn's)
     const int T = R + P;
-    if (blockIdx.x == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
+    if (wid == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
     // env of job j of queue q
     // (only the inclusive prefix sums stay live across the jobs: the shard of
     // job j is the number of shards whose prefix ends at or before j)
@@ -1943,7 +1944,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     // block index, the next ones are claimed once it is free (a slow reset
     // never holds up a job another worker could take): worker w claims on
     // shard x = w % kClaimShards, whose n-th claim is job G + x + kClaimShards * n.
-    int idx = blockIdx.x, nx = 0;
+    int idx = wid, nx = 0;
     for (;;) {
         // (the arguments afresh for each job: nothing of them stays live across
         // jobs; so is the lane index, or every lane mask derived from it -- the
@@ -1960,7 +1961,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             if (J.c.diag && lane == 0 && (spst & 3) == SPAWN_READY) DIAG_ADD(g_spawn_hits);
             if (idx < 128) OBSPROF(idx, lane);
             const int ps = idx < 128 ? idx : -1;
-            do_reset<MS, JL, SLICE && JL>(J.c, J.st, J.o, e, mt, lds, blockIdx.x, spst, lane, ps);
+            do_reset<MS, JL, SLICE && JL>(J.c, J.st, J.o, e, mt, lds, wid, spst, lane, ps);
             if (idx < 128) OBSPROF(128 + idx, lane);
         } else if (!RO && idx < R + P) {
             if (J.c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
@@ -1971,7 +1972,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             if (!SLICE || __builtin_amdgcn_s_memrealtime() < deadline) {   // (else: queued again next step)
                 if (J.c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
                 if (j < 128) OBSPROF(512 + j, lane);
-                do_spawn<MS, JL, SLICE && JL>(J.c, J.st, e, lds, blockIdx.x, JL ? deadline : 0ull, lane);
+                do_spawn<MS, JL, SLICE && JL>(J.c, J.st, e, lds, wid, JL ? deadline : 0ull, lane);
                 if (j < 128) OBSPROF(640 + j, lane);
             }
         }
@@ -1998,6 +1999,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
             for (int q = lane; q < kQCount; q += kWave)
                 if (!c.bg || q < kQShards || (q >= kQClaim && q <= kQDone)) qc[q * kQSpread] = 0;
     }
+}
+
+template <int MS, bool SLICE, bool RO, bool JL>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KArgs)
+{
+    autoreset_worker<MS, SLICE, RO, JL>((int)blockIdx.x, (int)gridDim.x);
 }
 
 // Background spawn-ahead (KCfg.bg): the step's spawn-ahead jobs, run by
@@ -2065,11 +2072,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
     }
 }
 
-__global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state st, const snake_out o)
+__device__ __forceinline__ void encode_one(const KCfg &c, const snake_state &st, const snake_out &o, const int e)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
-    const int e = blockIdx.x;
     const bool prof_ = (e & 511) == 0 && (e >> 9) < 128;
     if (prof_) OBSPROF(256 + (e >> 9), lane);
     // a reset env's obs is written by its reset; in every-step mode only the
@@ -2088,6 +2094,11 @@ __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state s
     if (prof_) OBSPROF(384 + (e >> 9), lane);
 }
 
+__global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state st, const snake_out o)
+{
+    encode_one(c, st, o, (int)blockIdx.x);
+}
+
 // k_encode over c.enc_per_wave consecutive envs per wave: the next env's grid
 // ring, current slot, crop centres and reset flag are loaded into registers
 // before this env's encode, so their memory round trip overlaps it (a
@@ -2095,7 +2106,7 @@ __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state s
 // latency- and occupancy-bound beside the reset workers). NPF = 16-byte ring
 // chunks per lane kept in flight (ring_bytes <= NPF * 1024).
 template <int NPF>
-__global__ void __launch_bounds__(64) k_encode_multi(const KCfg c, const snake_state st, const snake_out o)
+__device__ __forceinline__ void encode_multi(const KCfg &c, const snake_state &st, const snake_out &o, const int b)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
@@ -2105,7 +2116,7 @@ __global__ void __launch_bounds__(64) k_encode_multi(const KCfg c, const snake_s
     const int fs = c.fs, S = c.S, n16 = c.ring_bytes >> 4, fsS = fs * S;
     uint8_t *frames = lds + c.lds_frames;
     int *org = reinterpret_cast<int *>(lds + c.lds_centers);
-    const int e_begin = blockIdx.x * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
+    const int e_begin = b * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
     // (one vector value, not an array: an array of uint4 carried across the
     // loop was demoted to scratch)
     typedef uint32_t pf_t __attribute__((ext_vector_type(4 * NPF)));
@@ -2144,6 +2155,31 @@ __global__ void __launch_bounds__(64) k_encode_multi(const KCfg c, const snake_s
         }
     }
 #undef SNAKE_ENC_FETCH
+}
+
+template <int NPF>
+__global__ void __launch_bounds__(64) k_encode_multi(const KCfg c, const snake_state st, const snake_out o)
+{
+    encode_multi<NPF>(c, st, o, (int)blockIdx.x);
+}
+
+// The shared phase as one launch (KCfg.fused): blocks [0, reset_slots) are the
+// reset workers (autoreset_worker), the rest the encodes (NPF = 0: one env per
+// block, encode_one; else encode_multi<NPF>). Dispatched in block order, so the
+// workers go first as on the fork/join path, without the side stream's event
+// round trips on the host and on the device; the kernel's registers and LDS are
+// the larger of the two.
+template <int MS, int NPF>
+__global__ void __launch_bounds__(64) k_post(const KArgs)
+{
+    const int G = kargs().c.reset_slots, b = (int)blockIdx.x;
+    if (b < G) {
+        autoreset_worker<MS, false, false, true>(b, G);
+    } else {
+        const KArgs &A = kargs();
+        if constexpr (NPF == 0) encode_one(A.c, A.st, A.o, b - G);
+        else encode_multi<NPF>(A.c, A.st, A.o, b - G);
+    }
 }
 
 // Lean encode over c.enc_per_wave consecutive envs per workgroup of T threads
@@ -2586,6 +2622,29 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
         t3.close();
         return check_launch("k_encode");
+    }
+    if (k.fused && !k.bg && !k.spawn_budget && k.link_in_lds && !k.lean) {
+        // one launch on the caller's stream: workers, then encodes (k_post)
+        const int epw2 = k.enc_per_wave, n16 = k.ring_bytes >> 4;
+        const int npf = epw2 <= 1 ? 0 : (n16 <= kWave ? 1 : (n16 <= 2 * kWave ? 2 : 8));
+        const int enc_blocks = npf == 0 ? k.N : (k.N + epw2 - 1) / epw2;
+        const dim3 gp(k.reset_slots + enc_blocks);
+        const int lds_p = std::max(k.lds_bytes, k.lds_obs_bytes);
+        const KArgs a{k, st, o, nullptr};
+        TimedLaunch t2("k_post", sm);
+#define SNAKE_POST(MS_)                                                                          \
+        do {                                                                                     \
+            if (npf == 0) hipLaunchKernelGGL((k_post<MS_, 0>), gp, block, lds_p, sm, a);         \
+            else if (npf == 1) hipLaunchKernelGGL((k_post<MS_, 1>), gp, block, lds_p, sm, a);    \
+            else if (npf == 2) hipLaunchKernelGGL((k_post<MS_, 2>), gp, block, lds_p, sm, a);    \
+            else hipLaunchKernelGGL((k_post<MS_, 8>), gp, block, lds_p, sm, a);                  \
+        } while (0)
+        if (k.S <= 4) SNAKE_POST(4);
+        else if (k.S <= 8) SNAKE_POST(8);
+        else SNAKE_POST(16);
+#undef SNAKE_POST
+        t2.close();
+        return check_launch("k_post");
     }
     // fork: the resets and spawn-ahead jobs go first on the caller's stream
     // (dispatched the moment k_logic retires: dispatched second, behind the
