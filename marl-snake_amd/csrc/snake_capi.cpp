@@ -293,6 +293,14 @@ static bool bg_of(const snake_cfg *c, int64_t n_cand)
            2 * (n_cand + kWave) <= kJarrLdsMax;
 }
 
+// Queue entries per shard: k_logic's blocks of E envs spread over kQShards
+// shards, room for every env of a shard's blocks.
+static int64_t queue_cap(int64_t N, int64_t E)
+{
+    const int64_t blocks = (N + E - 1) / E;
+    return (blocks + kQShards - 1) / kQShards * E;
+}
+
 int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
 {
     int rc = check_cfg(c);
@@ -334,10 +342,8 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     }
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
         // kQShards) with room for every env of its blocks, + the step's counters
-        // (kQCount, each in its own line)
-        const int64_t E = kWave / (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
-        const int64_t blocks = (N + E - 1) / E;
-        const int64_t cap = (blocks + kQShards - 1) / kQShards * E;
+        // (kQCount, each in its own line); sized for any k_logic lane grouping
+        const int64_t cap = std::max(queue_cap(N, 4), std::max(queue_cap(N, 8), queue_cap(N, 16)));
         o->resetq = kQSets * (kNumQ * kQShards * cap + kQCounters) * 4;
     }
     o->obs = N * S * oh * ow * 8 * fs;
@@ -447,11 +453,19 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
 #define SNAKE_SPAWN_REDO_DEFAULT 0
 #endif
     k->spawn_redo = ev_redo ? (atoi(ev_redo) != 0) : SNAKE_SPAWN_REDO_DEFAULT;
-    k->q_envs_per_block = kWave / (k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16));
     {
-        const int64_t blocks = (N + k->q_envs_per_block - 1) / k->q_envs_per_block;
-        k->q_cap = (int)((blocks + kQShards - 1) / kQShards * k->q_envs_per_block);
+        // k_logic's lanes per env (4, 8 or 16 >= S; 64 / that = envs per wave):
+        // the fewest lanes that hold S snakes; small batches at least 8 (more,
+        // shorter waves: cfg2's 4 096 envs k_logic 16.4 -> 15.3 us, step 0.0540
+        // -> 0.0527 ms; 16 lanes 18.0 us; at cfg3 8 lanes cost 6 us). SNAKE_LOGIC_MS
+        // overrides.
+        const int ms_min = k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16);
+        static const char *ev_ms = getenv("SNAKE_LOGIC_MS");
+        const int ms = ev_ms ? atoi(ev_ms) : (N <= 8192 ? 8 : 0);
+        k->logic_ms = (ms == 4 || ms == 8 || ms == 16) && ms >= ms_min ? ms : ms_min;
     }
+    k->q_envs_per_block = kWave / k->logic_ms;
+    k->q_cap = (int)queue_cap(N, k->q_envs_per_block);
     k->spawn_thr = spawn_thr_of(c);
     // spawn-ahead time slice (spawn_budget_us above)
     k->draws_stride = lay.spawn_draws ? (int)round_up(lay.n_cand, 8) : 0;

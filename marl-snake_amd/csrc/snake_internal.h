@@ -72,7 +72,8 @@ struct KCfg {
     uint32_t mag_W;             // x / W == umulhi(x, mag_W) for cell indices x < H*W
     uint32_t mag_n16;           // q / (grid_stride/16) == umulhi(q, mag_n16) for q < 2^32/n16
     int reset_slots;            // min(N, kResetSlots)
-    int q_envs_per_block;       // envs per k_logic block (64 / MS)
+    int logic_ms;               // k_logic's lanes per env (its MS: 4, 8 or 16, >= S)
+    int q_envs_per_block;       // envs per k_logic block (64 / logic_ms)
     int q_cap;                  // queue entries per shard
     int spawn_thr;              // queue spawn-ahead when <= this many snakes live (-1: off)
     int spawn_prio;             // wave priority of the spawn-ahead jobs (resets: 3)

@@ -2169,12 +2169,12 @@ __global__ void __launch_bounds__(64) k_encode_multi(const KCfg c, const snake_s
 // workers go first as on the fork/join path, without the side stream's event
 // round trips on the host and on the device; the kernel's registers and LDS are
 // the larger of the two.
-template <int MS, int NPF>
+template <int MS, int NPF, bool RO>
 __global__ void __launch_bounds__(64) k_post(const KArgs)
 {
     const int G = kargs().c.reset_slots, b = (int)blockIdx.x;
     if (b < G) {
-        autoreset_worker<MS, false, false, true>(b, G);
+        autoreset_worker<MS, false, RO, true>(b, G);
     } else {
         const KArgs &A = kargs();
         if constexpr (NPF == 0) encode_one(A.c, A.st, A.o, b - G);
@@ -2585,7 +2585,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     const hipStream_t sm = (hipStream_t)stream;
     DeviceGuard dg(sm);
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
-    const int ms = k.S <= 4 ? 4 : (k.S <= 8 ? 8 : 16), epw = kWave / ms;   // envs per k_logic wave
+    const int ms = k.logic_ms, epw = kWave / ms;   // envs per k_logic wave
     const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits + epw * ms * kRespawnT * 4 + epw * ms * 2;
     const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
     BgCtx *bgc = nullptr;
@@ -2623,43 +2623,11 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         t3.close();
         return check_launch("k_encode");
     }
-    if (k.fused && !k.bg && !k.spawn_budget && k.link_in_lds && !k.lean) {
-        // one launch on the caller's stream: workers, then encodes (k_post)
-        const int epw2 = k.enc_per_wave, n16 = k.ring_bytes >> 4;
-        const int npf = epw2 <= 1 ? 0 : (n16 <= kWave ? 1 : (n16 <= 2 * kWave ? 2 : 8));
-        const int enc_blocks = npf == 0 ? k.N : (k.N + epw2 - 1) / epw2;
-        const dim3 gp(k.reset_slots + enc_blocks);
-        const int lds_p = std::max(k.lds_bytes, k.lds_obs_bytes);
-        const KArgs a{k, st, o, nullptr};
-        TimedLaunch t2("k_post", sm);
-#define SNAKE_POST(MS_)                                                                          \
-        do {                                                                                     \
-            if (npf == 0) hipLaunchKernelGGL((k_post<MS_, 0>), gp, block, lds_p, sm, a);         \
-            else if (npf == 1) hipLaunchKernelGGL((k_post<MS_, 1>), gp, block, lds_p, sm, a);    \
-            else if (npf == 2) hipLaunchKernelGGL((k_post<MS_, 2>), gp, block, lds_p, sm, a);    \
-            else hipLaunchKernelGGL((k_post<MS_, 8>), gp, block, lds_p, sm, a);                  \
-        } while (0)
-        if (k.S <= 4) SNAKE_POST(4);
-        else if (k.S <= 8) SNAKE_POST(8);
-        else SNAKE_POST(16);
-#undef SNAKE_POST
-        t2.close();
-        return check_launch("k_post");
-    }
-    // fork: the resets and spawn-ahead jobs go first on the caller's stream
-    // (dispatched the moment k_logic retires: dispatched second, behind the
-    // encodes' 64K waves, they would wait for LDS), the encodes follow on the
-    // side stream; join before return. SNAKE_ENCODE_ON_MAIN=1 swaps the two
-    // (A/B probe: 0.155 vs 0.135 ms per step for cfg3).
-    SideCtx sc;
-    if ((rc = side_ctx(sm, dg.dev, &sc))) return rc;
-    if (hipEventRecord(sc.fork, sm) != hipSuccess || hipStreamWaitEvent(sc.side, sc.fork, 0) != hipSuccess) {
-        set_error("fork to the side stream failed");
-        return SNAKE_E_LAUNCH;
-    }
-    if (bgc) {
-        // this step's spawn kernel on the background stream, not joined
-        if (hipStreamWaitEvent(bgc->x, sc.fork, 0) != hipSuccess) {
+    // this step's spawn kernel (background spawn-ahead) on the background
+    // stream once `fork` (recorded on the caller's stream after k_logic) has
+    // passed; not joined
+    auto launch_spawn = [&](hipEvent_t fork) -> int {
+        if (hipStreamWaitEvent(bgc->x, fork, 0) != hipSuccess) {
             set_error("ordering the background spawn kernel failed");
             return SNAKE_E_LAUNCH;
         }
@@ -2673,14 +2641,64 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         else if (k.S <= 8) hipLaunchKernelGGL(k_spawn<8>, gs, block, lds_sp, bgc->x, sa);
         else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bgc->x, sa);
         t4.close();
-        if ((rc = check_launch("k_spawn"))) return rc;
+        if (int rc2 = check_launch("k_spawn")) return rc2;
         if (hipEventRecord(bgc->done[k.qpar], bgc->x) != hipSuccess) {
             set_error("background spawn event failed");
             return SNAKE_E_LAUNCH;
         }
         bgc->pending[k.qpar] = true;
         bgc->steps++;
+        return SNAKE_OK;
+    };
+    SideCtx sc;
+    if ((rc = side_ctx(sm, dg.dev, &sc))) return rc;
+    if (k.fused && !k.spawn_budget && k.link_in_lds && !k.lean) {
+        // one launch on the caller's stream: workers, then encodes (k_post);
+        // with background spawn-ahead the workers run the resets only (RO)
+        if (bgc) {
+            if (hipEventRecord(sc.fork, sm) != hipSuccess) {
+                set_error("fork to the background stream failed");
+                return SNAKE_E_LAUNCH;
+            }
+            if ((rc = launch_spawn(sc.fork))) return rc;
+        }
+        const int epw2 = k.enc_per_wave, n16 = k.ring_bytes >> 4;
+        const int npf = epw2 <= 1 ? 0 : (n16 <= kWave ? 1 : (n16 <= 2 * kWave ? 2 : 8));
+        const int enc_blocks = npf == 0 ? k.N : (k.N + epw2 - 1) / epw2;
+        const dim3 gp(k.reset_slots + enc_blocks);
+        const int lds_p = std::max(k.lds_bytes, k.lds_obs_bytes);
+        const KArgs a{k, st, o, nullptr};
+        TimedLaunch t2("k_post", sm);
+#define SNAKE_POST(MS_, RO_)                                                                          \
+        do {                                                                                          \
+            if (npf == 0) hipLaunchKernelGGL((k_post<MS_, 0, RO_>), gp, block, lds_p, sm, a);         \
+            else if (npf == 1) hipLaunchKernelGGL((k_post<MS_, 1, RO_>), gp, block, lds_p, sm, a);    \
+            else if (npf == 2) hipLaunchKernelGGL((k_post<MS_, 2, RO_>), gp, block, lds_p, sm, a);    \
+            else hipLaunchKernelGGL((k_post<MS_, 8, RO_>), gp, block, lds_p, sm, a);                  \
+        } while (0)
+        if (k.bg) {
+            if (k.S <= 4) SNAKE_POST(4, true);
+            else if (k.S <= 8) SNAKE_POST(8, true);
+            else SNAKE_POST(16, true);
+        } else {
+            if (k.S <= 4) SNAKE_POST(4, false);
+            else if (k.S <= 8) SNAKE_POST(8, false);
+            else SNAKE_POST(16, false);
+        }
+#undef SNAKE_POST
+        t2.close();
+        return check_launch("k_post");
     }
+    // fork: the resets and spawn-ahead jobs go first on the caller's stream
+    // (dispatched the moment k_logic retires: dispatched second, behind the
+    // encodes' 64K waves, they would wait for LDS), the encodes follow on the
+    // side stream; join before return. SNAKE_ENCODE_ON_MAIN=1 swaps the two
+    // (A/B probe: 0.155 vs 0.135 ms per step for cfg3).
+    if (hipEventRecord(sc.fork, sm) != hipSuccess || hipStreamWaitEvent(sc.side, sc.fork, 0) != hipSuccess) {
+        set_error("fork to the side stream failed");
+        return SNAKE_E_LAUNCH;
+    }
+    if (bgc && (rc = launch_spawn(sc.fork))) return rc;
     static const bool resets_main = !(getenv("SNAKE_ENCODE_ON_MAIN") && atoi(getenv("SNAKE_ENCODE_ON_MAIN")));
     const hipStream_t s_res = resets_main ? sm : sc.side, s_enc = resets_main ? sc.side : sm;
     auto launch_resets = [&]() {
