@@ -187,13 +187,16 @@ class SnakeVecEnv:
             check(self._L.snake_sync(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs,
                                      self._stream()))
 
-    # Outputs of one call (include/snake_env.h snake_out): the observations in a
-    # fresh allocation of their own (a bare observation buffer that the caller
-    # drops is the one the next step gets back), every other output a view of
-    # ONE fresh slab -- fresh per step (train_dqn.py:297 keeps references to
-    # returned observations), two allocator calls instead of seven.
+    # Outputs of one call (include/snake_env.h snake_out): the observations,
+    # rewards and dones -- returned every step -- in fresh allocations of their
+    # own (a buffer the caller drops is the one the next step gets back: an
+    # allocation costs about as much as one view op, and a slab view of a typed
+    # output takes three), the info outputs views of ONE fresh slab, made only
+    # when read. Fresh per step (train_dqn.py:297 keeps references to returned
+    # observations): four allocator calls instead of seven.
     # (name, dtype, per-env shape) in C-ABI order.
     _OUTS = ('obs', 'rew', 'done', 'ep_done', 'rank', 'ep_stats', 'err')
+    _OWN = ('obs', 'rew', 'done')
 
     def _plan_slab(self):
         torch = _torch()
@@ -205,7 +208,7 @@ class SnakeVecEnv:
         for k in self._OUTS:
             dt, shp = spec[k]
             n = N * int(np.prod(shp, dtype=np.int64)) * torch.empty((), dtype=dt).element_size()
-            if k == 'obs':
+            if k in self._OWN:
                 plan[k] = (0, n, dt, (N,) + tuple(shp))
                 continue
             plan[k] = (off, n, dt, (N,) + tuple(shp))
@@ -215,18 +218,24 @@ class SnakeVecEnv:
         self._so = SnakeOut()
 
     def _new_out(self):
-        """((obs, slab), SnakeOut with their pointers); views via _view."""
+        """((obs, slab, rew, done), SnakeOut with their pointers); views via _view."""
         torch = _torch()
-        obs = torch.empty(self._obs_shape_n, dtype=torch.uint8, device=self.device)
-        slab = torch.empty(self._slab_bytes, dtype=torch.uint8, device=self.device)
-        base, so, plan = slab.data_ptr(), self._so, self._slab_plan
-        so.obs = obs.data_ptr()
-        so.rew, so.done, so.ep_done, so.rank, so.ep_stats, so.err = (base + plan[k][0] for k in self._OUTS[1:])
-        return (obs, slab), so
+        dev, plan = self.device, self._slab_plan
+        obs = torch.empty(self._obs_shape_n, dtype=torch.uint8, device=dev)
+        rew = torch.empty(plan['rew'][3], dtype=torch.float64, device=dev)
+        done = torch.empty(plan['done'][3], dtype=torch.bool, device=dev)
+        slab = torch.empty(self._slab_bytes, dtype=torch.uint8, device=dev)
+        base, so = slab.data_ptr(), self._so
+        so.obs, so.rew, so.done = obs.data_ptr(), rew.data_ptr(), done.data_ptr()
+        so.ep_done, so.rank, so.ep_stats, so.err = (base + plan[k][0] for k in self._OUTS[3:])
+        return (obs, slab, rew, done), so
+
+    _OWN_AT = {'obs': 0, 'rew': 2, 'done': 3}
 
     def _view(self, bufs, k):
-        if k == 'obs':
-            return bufs[0]
+        i = self._OWN_AT.get(k)
+        if i is not None:
+            return bufs[i]
         off, n, dt, shape = self._slab_plan[k]
         v = bufs[1][off:off + n]
         return (v if dt == _torch().uint8 else v.view(dt)).view(shape)
@@ -301,7 +310,7 @@ class SnakeVecEnv:
                 raise KeyError(f'invalid action for an alive snake in envs {bad[:8]}')
             raise RuntimeError(f'auto-reset gave up placing disjoint snakes in envs '
                                f'{(err == 2).nonzero().flatten().tolist()[:8]}')
-        return self._view(slab, 'obs'), self._view(slab, 'rew'), self._view(slab, 'done'), info
+        return slab[0], slab[2], slab[3], info
 
     def render_rgb(self):
         """rgb_from_grid of every env's current grid (grid_util.py:164-175), on the
