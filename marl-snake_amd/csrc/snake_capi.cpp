@@ -483,6 +483,8 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         // the shared phase as one launch (k_post) where it applies: in-step
         // spawn-ahead, the LDS draw record, the staged encodes
         // (cfg3 0.0970 -> 0.0941 ms per step, cfg2 0.0591 -> 0.0539, same box)
+        static const char *ev_r1 = getenv("SNAKE_ROWS1");
+        k->rows1 = ev_r1 ? atoi(ev_r1) : 0;
         static const char *ev_fu = getenv("SNAKE_FUSED");
         k->fused = ev_fu ? atoi(ev_fu) : 1;
         if (bg_of(c, lay.n_cand) != (k->bg != 0)) {

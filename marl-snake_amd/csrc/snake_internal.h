@@ -68,6 +68,7 @@ struct KCfg {
     // staged group (0: direct encode), the buffer, and magic reciprocals of
     // fs*oh and oh (x / d == umulhi(x, m) for the row indices used)
     int enc_group, lds_stage;
+    int rows1;                  // one-frame stacks: encode_rows1 (dword row reads, whole-cell stores)
     uint32_t mag_fsoh, mag_oh;
     uint32_t mag_W;             // x / W == umulhi(x, mag_W) for cell indices x < H*W
     uint32_t mag_n16;           // q / (grid_stride/16) == umulhi(q, mag_n16) for q < 2^32/n16

@@ -912,10 +912,75 @@ __device__ void encode_rows(const KCfg &c, const uint8_t *frames, const int *org
     }
 }
 
+// Row-wise encode of a one-frame stack (fs == 1), with few LDS instructions:
+// lane = one (snake, window row), whose ow output cells are 8*ow contiguous
+// bytes of the staged image. The row's grid bytes come in as dwords (two
+// per 4 cells, realigned with v_alignbyte), each cell's 8 channels are built in
+// a register pair, branch-free, and stored whole (one ds_write_b64 per cell),
+// so the stage needs no zeroing pass and no per-cell byte stores; cells outside
+// the grid write zeros. encode_rows does the same with one LDS byte read and
+// (non-empty cells) one byte store per cell plus a zeroing pass: about 2.5x the
+// LDS instructions, which the concurrent reset workers compete for.
+#ifndef SNAKE_ROWS1
+#define SNAKE_ROWS1 1
+#endif
+__device__ void encode_rows1(const KCfg &c, const uint8_t *frames, const int *org, uint8_t *obs_env,
+                             uint8_t *stage, int lane)
+{
+    const int ow = c.ow, oh = c.oh, S = c.S, W = c.W, H = c.H;
+    const int rowb = ow * 8, P = oh * rowb;
+    const int nd = c.grid_stride >> 2;   // frame dwords (reads are clamped into the frame)
+    const uint32_t *f32 = reinterpret_cast<const uint32_t *>(frames);
+    const bool wide = (c.units & 1) == 0;
+    for (int k0 = 0; k0 < S; k0 += c.enc_group) {
+        const int gs = min(c.enc_group, S - k0), bytes = gs * P;
+        for (int rr = lane; rr < gs * oh; rr += kWave) {
+            const int kk = (int)__umulhi((uint32_t)rr, c.mag_oh), i = rr - kk * oh;
+            const int k = k0 + kk;
+            const int p = org[k];
+            const int r = (p >> 16) - 256 + i, c0 = (p & 0xffff) - 256;
+            const bool rok = (unsigned)r < (unsigned)H;
+            const int a = r * W + c0;          // grid byte of window cell 0
+            const int d0 = a >> 2;              // (floor: a may be negative)
+            const uint32_t sh = (uint32_t)(a & 3);   // (alignbyte shifts by bytes)
+            uint8_t *dst = stage + kk * P + i * rowb;
+            uint32_t lo_w = f32[min(max(d0, 0), nd - 1)];
+            for (int jb = 0; jb < ow; jb += 4) {
+                const uint32_t hi_w = f32[min(max(d0 + (jb >> 2) + 1, 0), nd - 1)];
+                const uint32_t w = __builtin_amdgcn_alignbyte(hi_w, lo_w, sh);   // grid bytes a+jb .. a+jb+3
+                lo_w = hi_w;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int j = jb + u, col = c0 + j;
+                    const int v = (rok && (unsigned)col < (unsigned)W) ? (int)((w >> (8 * u)) & 255u) : 0;
+                    const int id = div10(v), code = v - 10 * id;
+                    const int ch = (v < 3) ? v - 1 : code - 1 + ((id == k) ? 3 : 0);
+                    const uint32_t bit = (uint32_t)min(v, 1) << (8 * (ch & 3));
+                    uint2 cell;
+                    cell.x = ch < 4 ? bit : 0u;
+                    cell.y = ch < 4 ? 0u : bit;
+                    if (j < ow) *reinterpret_cast<uint2 *>(dst + j * 8) = cell;
+                }
+            }
+        }
+        wave_sync();
+        uint8_t *out = obs_env + (int64_t)k0 * P;
+        if (wide) {
+            for (int q = lane; q < bytes >> 4; q += kWave)
+                reinterpret_cast<uint4 *>(out)[q] = reinterpret_cast<const uint4 *>(stage)[q];
+        } else {
+            for (int q = lane; q < bytes >> 3; q += kWave)
+                reinterpret_cast<uint2 *>(out)[q] = reinterpret_cast<const uint2 *>(stage)[q];
+        }
+        wave_sync();
+    }
+}
+
 __device__ __forceinline__ void encode_obs(const KCfg &c, const uint8_t *frames, const int *org, int slot0,
                                            uint8_t *obs_env, uint8_t *lds, int lane)
 {
-    if (c.enc_group > 0) encode_rows(c, frames, org, slot0, obs_env, lds + c.lds_stage, lane);
+    if (SNAKE_ROWS1 && c.enc_group > 0 && c.fs == 1 && c.rows1) encode_rows1(c, frames, org, obs_env, lds + c.lds_stage, lane);
+    else if (c.enc_group > 0) encode_rows(c, frames, org, slot0, obs_env, lds + c.lds_stage, lane);
     else encode(c, frames, org, slot0, obs_env, lane);
 }
 
