@@ -239,13 +239,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // NT = output channels / 16 (2: conv1, 4: conv2/conv3). Wave w takes column
 // tile w % NT and 16*NT/... row tiles: NT == 4 -> all 8 row tiles, NT == 2 ->
-// row tiles 4*(w/2) .. +3.
-template <int MODE, int NT>
+// row tiles 4*(w/2) .. +3. WT (NT == 4 only): wave tiles of 4 row x 2 column
+// tiles instead -- wave w takes column tiles 2*(w%2), +1 and row tiles
+// 4*(w/2) .. +3: each A fragment feeds two MFMAs (half the LDS reads per MFMA),
+// each block loads two B fragments.
+template <int MODE, int NT, bool WT = false>
 __global__ void __launch_bounds__(256) k_conv32_mfma(const GemmArgs g)
 {
+    static_assert(!WT || NT == 4, "wave tiles of 4 x 2 need four column tiles");
     extern __shared__ __attribute__((aligned(16))) float patch[];
     __shared__ int offs[4 * 76];   // K <= 9 * 128: 72 blocks + padding + 1
-    constexpr int RT = NT == 4 ? 8 : 4;   // row tiles per wave
+    constexpr int RT = WT ? 4 : (NT == 4 ? 8 : 4);   // row tiles per wave
+    constexpr int CT = WT ? 2 : 1;                   // column tiles per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int H = g.H, W = g.W, C = g.C, K = g.K, N = g.N;
     const int W2 = W + 2, CS = conv_cell_stride(C), P = H * W;
@@ -306,8 +311,8 @@ __global__ void __launch_bounds__(256) k_conv32_mfma(const GemmArgs g)
     }
     __syncthreads();
     // ---- this wave's tiles
-    const int ct = wave % NT;
-    const int rt0 = NT == 4 ? 0 : 4 * (wave / 2);
+    const int ct = WT ? 2 * (wave & 1) : wave % NT;
+    const int rt0 = WT ? 4 * (wave >> 1) : (NT == 4 ? 0 : 4 * (wave / 2));
     const int grp = lane >> 4, l16 = lane & 15;
     int abase[RT];   // LDS 16-byte index of each row tile's lane-row cell (tap (1,1), channel 0)
 #pragma unroll
@@ -319,11 +324,18 @@ __global__ void __launch_bounds__(256) k_conv32_mfma(const GemmArgs g)
         const int r = (int)(b * (H + 1) + y + 1 - t0);
         abase[i] = ((r * W2 + x + 1) * CS) >> 2;
     }
-    const int col = ct * 16 + l16;
-    const float *wrow = g.w + (int64_t)col * K;
-    f32x4 acc[RT];
+    int col[CT];
+    const float *wrow[CT];
 #pragma unroll
-    for (int i = 0; i < RT; i++) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < CT; c++) {
+        col[c] = (ct + c) * 16 + l16;
+        wrow[c] = g.w + (int64_t)col[c] * K;
+    }
+    f32x4 acc[RT][CT];
+#pragma unroll
+    for (int i = 0; i < RT; i++)
+#pragma unroll
+        for (int c = 0; c < CT; c++) acc[i][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // per 16-k block and lane group: the LDS offset (in 16-byte units) of its
     // (tap, channel) from a row's centre cell; blocks are processed kRing at a
     // time, and k past K (the padding blocks, one extra entry for the last
@@ -345,9 +357,12 @@ __global__ void __launch_bounds__(256) k_conv32_mfma(const GemmArgs g)
     // A: the next block's fragments are read before this block's MFMAs
     const f32x4 *patch4 = reinterpret_cast<const f32x4 *>(patch);
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    f32x4 bq[kRing];
+    f32x4 bq[kRing][CT];
 #pragma unroll
-    for (int d = 0; d < kRing; d++) bq[d] = *reinterpret_cast<const f32x4 *>(wrow + min(16 * d + 4 * grp, K - 4));
+    for (int d = 0; d < kRing; d++)
+#pragma unroll
+        for (int c = 0; c < CT; c++)
+            bq[d][c] = *reinterpret_cast<const f32x4 *>(wrow[c] + min(16 * d + 4 * grp, K - 4));
     f32x4 a[RT];
     {
         const int off = offs[grp];
@@ -357,15 +372,19 @@ __global__ void __launch_bounds__(256) k_conv32_mfma(const GemmArgs g)
     // two blocks per iteration: the B ring and the A fragments ping-pong
     // between fixed registers (a register copy would wait for the load it copies)
     f32x4 a2[RT];
-    auto block = [&](int kb, f32x4 (&acur)[RT], f32x4 (&anext)[RT], f32x4 &bslot) {
+    auto block = [&](int kb, f32x4 (&acur)[RT], f32x4 (&anext)[RT], f32x4 (&bslot)[CT]) {
         const int off = offs[4 * (kb + 1) + grp];
 #pragma unroll
         for (int i = 0; i < RT; i++) anext[i] = patch4[abase[i] + off];
         // (conv2/conv3: K = 9 * 32 or 9 * 64, a multiple of 16 -- no mask, so
         // nothing ties the ring's loads to a select at issue time)
-        f32x4 bv = bslot;
-        if constexpr (MODE == kConvU8) bv = 16 * kb + 4 * grp < K ? bv : zero;
-        bslot = *reinterpret_cast<const f32x4 *>(wrow + min(16 * (kb + kRing) + 4 * grp, K - 4));
+        f32x4 bv[CT];
+#pragma unroll
+        for (int c = 0; c < CT; c++) {
+            bv[c] = bslot[c];
+            if constexpr (MODE == kConvU8) bv[c] = 16 * kb + 4 * grp < K ? bv[c] : zero;
+            bslot[c] = *reinterpret_cast<const f32x4 *>(wrow[c] + min(16 * (kb + kRing) + 4 * grp, K - 4));
+        }
         // (the loads stay issued ahead of this block's MFMAs: without the
         // barriers the scheduler sinks them next to their uses)
         __builtin_amdgcn_sched_barrier(0);
@@ -373,7 +392,9 @@ __global__ void __launch_bounds__(256) k_conv32_mfma(const GemmArgs g)
         for (int j = 0; j < 4; j++)
 #pragma unroll
             for (int i = 0; i < RT; i++)
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[i][j], bv[j], acc[i], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < CT; c++)
+                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[i][j], bv[c][j], acc[i][c], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
     };
     for (int kb = 0; kb < nbp; kb += 2) {
@@ -386,7 +407,9 @@ __global__ void __launch_bounds__(256) k_conv32_mfma(const GemmArgs g)
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int64_t m = m0 + (rt0 + i) * 16 + 4 * grp + r;
-            if (m < M) g.y[m * N + col] = acc[i][r];
+#pragma unroll
+            for (int c = 0; c < CT; c++)
+                if (m < M) g.y[m * N + col[c]] = acc[i][c][r];
         }
     }
 }
@@ -396,7 +419,13 @@ int conv_mfma(const GemmArgs &g, hipStream_t s, const char *what)
 {
     const int64_t lds = conv_patch_bytes(g.H, g.W, g.C);
     const dim3 grid((unsigned)((g.M + kConvRows - 1) / kConvRows));
-    hipLaunchKernelGGL((k_conv32_mfma<MODE, NT>), grid, dim3(256), (size_t)lds, s, g);
+    // 4 x 2 wave tiles for the 64-channel layers (20x20x8, 16 384 observations:
+    // conv2/conv3 3 715 -> 3 666 us per launch on average, forward 9.84 -> 9.75
+    // ms; parity green); SNAKE_DQN32_WT=0 selects the 8 x 1 tiles (A/B)
+    static const char *ev_wt = getenv("SNAKE_DQN32_WT");
+    static const bool wt = !ev_wt || atoi(ev_wt) != 0;
+    if (NT == 4 && wt) hipLaunchKernelGGL((k_conv32_mfma<MODE, 4, true>), grid, dim3(256), (size_t)lds, s, g);
+    else hipLaunchKernelGGL((k_conv32_mfma<MODE, NT>), grid, dim3(256), (size_t)lds, s, g);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) { set_error("%s launch failed: %s", what, hipGetErrorString(err)); return SNAKE_E_LAUNCH; }
     return SNAKE_OK;
