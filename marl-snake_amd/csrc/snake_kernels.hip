@@ -1188,7 +1188,12 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     wave_sync();
     const int nxt = __shfl(cell, (lane + 1) & 63);
     const int tailcell = __shfl(cell, min(lane + L - 1, 63));
-    const int pretail = __shfl(cell, min(lane + L - 2, 63));
+    // the tail queue holds the whole deque (up to 14 directions): entry j =
+    // directions[-1-j] = the direction of body cell L-2-j, on lane sk*L + L-2-j
+    const int mydir = dir_of_diff(cell - nxt, W);
+    const int nq0 = min(L - 1, 14);
+    uint32_t tq0 = 0;
+    for (int j = 0; j < nq0; j++) tq0 |= (uint32_t)__shfl(mydir, min(sk * L + L - 2 - j, 63)) << (2 * j);
     if (lane < SL) {
         const int v = (si == 0 ? C_HEAD : (si == L - 1 ? C_TAIL : C_BODY)) + 10 * sk;
         work[cell] = (uint8_t)v;
@@ -1202,7 +1207,7 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
             rec.y = dir_of_diff(cell - nxt, W) | (1 << 8);
             rec.z = 0 | ((L - 1) << 16);
             // cached directions[-1] (the direction move() pops next)
-            rec.w = dir_of_diff(pretail - tailcell, W) | (1 << 28);   // tail queue: directions[-1] only
+            rec.w = (int)(tq0 | ((uint32_t)nq0 << 28));
             reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + sk] = rec;
             const int og = pack_origin(c, hr, hc);
             for (int f = 0; f < c.fs; f++) {
@@ -1386,7 +1391,11 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     // per byte offset), and the tail end is read as aligned 8-byte chunks into a
     // queue in rec.w (entry 0 = directions[-1], then directions[-2], ...; count
     // in bits 28-31). One byte store and one line fetch per snake and step
-    // were the largest share of k_logic's traffic.
+    // were the largest share of k_logic's traffic. A queue whose count equals
+    // rl holds the whole deque (every snake of up to 14 directions, i.e. all
+    // fresh ones): it is kept whole by appending each step's new head direction
+    // and never refills from the ring -- a refill every 2-3 steps for a short
+    // snake, in the same step for every env after a reset of all of them.
     uint32_t tq = (uint32_t)rec.w;
     const int tdir = (int)(tq & 3u);          // directions[-1] (core/snake.py:103)
     int hbuf = (rec.y >> 16) & 255;
@@ -1501,7 +1510,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     if (pn && lane == 0) nbase = atomicAdd(&qcnt[(2 * kQShards + shard) * kQSpread], __popcll(pn));
 
     uint8_t *ring = st.body + ((int64_t)e * S + k) * cap;
-    const bool refill = alive && !eat && (tq >> 28) == 1u;
+    const uint32_t tcnt0 = tq >> 28;
+    const bool tfull = (int)tcnt0 == rl;   // the queue holds the whole deque
+    const bool refill = alive && !eat && tcnt0 == 1u && !tfull;
     const int rt1 = (((rh - 1) & (cap - 1)) + rl - 1) & (cap - 1), rbase = rt1 & ~7;
     uint64_t rchunk = 0;
     if (refill) rchunk = *reinterpret_cast<const uint64_t *>(ring + rbase);
@@ -1566,7 +1577,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
             ntc = tc + dir_dc(tdir);
             const uint32_t cnt = (tq >> 28) - 1u;
             tq = ((tq & 0x0fffffffu) >> 2) | (cnt << 28);
-            if (cnt == 0u) {
+            if (tfull) {
+                tq = (tq & 0x0fffffffu) | ((uint32_t)dir << (2 * cnt)) | ((cnt + 1u) << 28);   // the new directions[0]
+            } else if (cnt == 0u) {
                 // refill from the chunk holding the new directions[-1] (position t):
                 // t, t-1, .. down to the chunk start, but not below the head (the
                 // positions past it are free ring slots); pending head-word bytes
@@ -1585,6 +1598,8 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
                 tq = nq | ((uint32_t)n << 28);
             }
         } else {
+            if (tfull && tcnt0 < 14u)   // (a 15th entry does not fit: from then on the ring refills it)
+                tq = (tq & 0x0fffffffu) | ((uint32_t)dir << (2 * tcnt0)) | ((tcnt0 + 1u) << 28);
             rl++;
         }
         work[nhr * W + nhc] = (uint8_t)(C_HEAD + 10 * k);
