@@ -197,6 +197,24 @@ __device__ __forceinline__ int zero_bytes(uint32_t x)
     return __popc(t);
 }
 
+// Observation stores (the step's bulk output, 2/3 of its bytes) as
+// non-temporal stores (SNAKE_OBS_NT): streamed past the caches, so they do not
+// evict the env state the next step's k_logic reads.
+#ifndef SNAKE_OBS_NT
+#define SNAKE_OBS_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ void obs_store(T *p, const T &v)
+{
+#if SNAKE_OBS_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
 constexpr int kRespawnT = 4;   // raws per lane prefetched by the fast fruit respawn
 
 __device__ __forceinline__ uint32_t gen_mask(uint32_t m)
@@ -764,10 +782,10 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
             uint4 v;
             v.x = (uint32_t)a; v.y = (uint32_t)(a >> 32);
             v.z = (uint32_t)b; v.w = (uint32_t)(b >> 32);
-            *reinterpret_cast<uint4 *>(obs_env + 16 * (int64_t)p) = v;
+            obs_store(reinterpret_cast<v4u *>(obs_env + 16 * (int64_t)p), (v4u){v.x, v.y, v.z, v.w});
         } else {
-            *reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p) = a;
-            if (has_b) *reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p + 8) = b;
+            obs_store(reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p), a);
+            if (has_b) obs_store(reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p + 8), b);
         }
         f += c.adv_f;
         if (f >= fs) { f -= fs; j++; }
@@ -824,7 +842,7 @@ __device__ void encode_lean(const KCfg &c, const uint8_t *pf, const int *base, i
                 kk += ci;
             }
         }
-        reinterpret_cast<uint4 *>(obs_env)[p] = make_uint4(w[0], w[1], w[2], w[3]);
+        obs_store(reinterpret_cast<v4u *>(obs_env) + p, (v4u){w[0], w[1], w[2], w[3]});
     }
 }
 
@@ -903,10 +921,10 @@ __device__ void encode_rows(const KCfg &c, const uint8_t *frames, const int *org
         uint8_t *out = obs_env + (int64_t)k0 * P;
         if (wide) {
             for (int q = lane; q < bytes >> 4; q += kWave)
-                reinterpret_cast<uint4 *>(out)[q] = reinterpret_cast<const uint4 *>(stage)[q];
+                obs_store(reinterpret_cast<v4u *>(out) + q, reinterpret_cast<const v4u *>(stage)[q]);
         } else {
             for (int q = lane; q < bytes >> 3; q += kWave)
-                reinterpret_cast<uint2 *>(out)[q] = reinterpret_cast<const uint2 *>(stage)[q];
+                obs_store(reinterpret_cast<v2u *>(out) + q, reinterpret_cast<const v2u *>(stage)[q]);
         }
         wave_sync();
     }
@@ -967,10 +985,10 @@ __device__ void encode_rows1(const KCfg &c, const uint8_t *frames, const int *or
         uint8_t *out = obs_env + (int64_t)k0 * P;
         if (wide) {
             for (int q = lane; q < bytes >> 4; q += kWave)
-                reinterpret_cast<uint4 *>(out)[q] = reinterpret_cast<const uint4 *>(stage)[q];
+                obs_store(reinterpret_cast<v4u *>(out) + q, reinterpret_cast<const v4u *>(stage)[q]);
         } else {
             for (int q = lane; q < bytes >> 3; q += kWave)
-                reinterpret_cast<uint2 *>(out)[q] = reinterpret_cast<const uint2 *>(stage)[q];
+                obs_store(reinterpret_cast<v2u *>(out) + q, reinterpret_cast<const v2u *>(stage)[q]);
         }
         wave_sync();
     }
