@@ -435,7 +435,10 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     static const char *ev_prio = getenv("SNAKE_SPAWN_PRIO");
     const int slots = ev_slots ? std::max(1, std::min(kResetSlots, atoi(ev_slots))) : kResetSlots;
     k->reset_slots = (int)std::min<int64_t>(N, slots);
-    k->spawn_prio = ev_prio ? std::max(0, std::min(3, atoi(ev_prio))) : 1;
+    // spawn-ahead jobs at 1, below the encodes; small batches with in-step
+    // spawn-ahead at 3 (a lone attempt is there the step's critical path: cfg2
+    // 0.0510 -> 0.0494 ms; at cfg3 it costs 0.0905 -> 0.0960)
+    k->spawn_prio = ev_prio ? std::max(0, std::min(3, atoi(ev_prio))) : (N <= 8192 && !bg_of(c, n_cand) ? 3 : 1);
     // k_encode above the spawn-ahead jobs: the bandwidth-bound encodes then keep
     // HBM busy while the compute-bound workers fill the issue gaps (SNAKE_ENCODE_PRIO,
     // default 2: step 0.1275 -> 0.1200 ms at cfg3; 0 = hardware default). With
