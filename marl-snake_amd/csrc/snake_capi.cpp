@@ -330,7 +330,10 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     // perm_trace): the u16 draw record in LDS up to kJarrLdsMax bytes, else one
     // global u32 link table per reset worker.
     const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
-    o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax) ? 0 : std::min<int64_t>(N, kResetSlots) * link;
+    // (background spawn-ahead boards too: k_post_lean's workers keep no draw
+    // record in LDS, a reset without a ready record uses its link table)
+    o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax && !bg_of(c, o->n_cand))
+                      ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     // (background spawn-ahead: two records per env, see k_spawn)
     o->spawn = (bg_of(c, o->n_cand) ? 2 : 1) * N * kSpawnStride * 4;
     // paused spawn-ahead attempts keep their draws here (u16 per draw index):
@@ -417,6 +420,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         }
         k->enc_group = g;
         k->lds_stage = off;
+        k->lds_worker = off;   // (frames, centres, fruit buffer: a resets-only worker without the draw record)
         if (g > 0) off += (int)round_up(g * P, 16);
         const uint64_t fsoh = (uint64_t)k->fs * k->oh, oh = (uint64_t)k->oh;
         k->mag_fsoh = (uint32_t)(((1ull << 32) + fsoh - 1) / fsoh);
@@ -488,6 +492,10 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         // (cfg3 0.0970 -> 0.0941 ms per step, cfg2 0.0591 -> 0.0539, same box)
         static const char *ev_r1 = getenv("SNAKE_ROWS1");
         k->rows1 = ev_r1 ? atoi(ev_r1) : 0;
+        // background spawn-ahead with four-wave lean encodes as one launch
+        // (k_post_lean; cfg5 0.1227 -> 0.1169 ms, same box)
+        static const char *ev_pl = getenv("SNAKE_POST_LEAN");
+        k->post_lean = ev_pl ? atoi(ev_pl) : 1;
         static const char *ev_fu = getenv("SNAKE_FUSED");
         k->fused = ev_fu ? atoi(ev_fu) : 1;
         if (bg_of(c, lay.n_cand) != (k->bg != 0)) {

@@ -88,6 +88,8 @@ struct KCfg {
     int enc_per_wave;           // envs per k_encode wave (1: k_encode, else k_encode_multi with prefetch)
     int bg;                     // 1: spawn-ahead jobs in the background kernel k_spawn (not k_autoreset)
     int fused;                  // 1: reset workers and encodes in one launch (k_post), no side stream
+    int post_lean;              // 1: background spawn-ahead + four-wave lean encodes in one launch (k_post_lean)
+    int lds_worker;             // k_post_lean: LDS bytes of one resets-only worker (no draw record)
     int qpar;                   // queue set of this step (0 unless bg)
     int spawn_slots;            // k_spawn workers
     int bg_tries;               // k_spawn: permutation attempts per job (until disjoint)

@@ -161,6 +161,15 @@ __device__ __forceinline__ uint32_t link_get(const gu32 *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A worker's global link table between its writers and its readers, all lanes
+// of one wave: the wave's stores and atomics complete at device scope, then a
+// wave barrier.
+__device__ __forceinline__ void link_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Direction (core/snake.py:33-37): 0 UP(-1,0) 1 RIGHT(0,1) 2 DOWN(1,0) 3 LEFT(0,-1)
 __device__ __forceinline__ int dir_dr(int d) { return d == 0 ? -1 : (d == 2 ? 1 : 0); }
 __device__ __forceinline__ int dir_dc(int d) { return d == 1 ? 1 : (d == 3 ? -1 : 0); }
@@ -1073,10 +1082,13 @@ __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, 
         lu16 *jsmall = (lu16 *)(lds + c.lds_fruit);   // the fruit buffer is free until place_fruits
         for (int x = 4 * lane; x < c.link_stride - kWave; x += 4 * kWave)
             *(gu4 *)(link + x) = (v4u32)kNoLink;
-        __syncthreads();
+        // (the table is this wave's alone: its own stores and atomics drained
+        // and made visible, no workgroup barrier -- k_post_lean runs four
+        // independent workers per workgroup)
+        link_sync();
         mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, lane, e);
         STAMP(e, lane, 2 + 3 * min(attempt, 3));
-        __syncthreads();   // the link table, written by every lane
+        link_sync();   // the link table, written by every lane
         perm_trace<MS>(S, link, jsmall, q, lane);
     }
     STAMP(e, lane, 3 + 3 * min(attempt, 3));
@@ -1998,10 +2010,9 @@ __device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st,
 // global link tables; one path per instantiation.
 // wid = this worker (0 .. G-1): k_autoreset's block, or a block of k_post.
 template <int MS, bool SLICE, bool RO, bool JL>
-__device__ __forceinline__ void autoreset_worker(const int wid, const int G)
+__device__ __forceinline__ void autoreset_worker(const int wid, const int G, uint8_t *lds)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
     const KArgs &A = kargs();
     const KCfg &c = A.c;
     const snake_state &st = A.st;
@@ -2049,7 +2060,7 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G)
         // MT word bounds, the scan steps -- would be held, spilled, for the whole
         // kernel instead of recomputed by one compare)
         const KArgs &J = kargs();
-        int lane = threadIdx.x;
+        int lane = threadIdx.x & (kWave - 1);
         __asm__ volatile("" : "+v"(lane));
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
@@ -2102,7 +2113,8 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G)
 template <int MS, bool SLICE, bool RO, bool JL>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KArgs)
 {
-    autoreset_worker<MS, SLICE, RO, JL>((int)blockIdx.x, (int)gridDim.x);
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    autoreset_worker<MS, SLICE, RO, JL>((int)blockIdx.x, (int)gridDim.x, lds);
 }
 
 // Background spawn-ahead (KCfg.bg): the step's spawn-ahead jobs, run by
@@ -2272,7 +2284,8 @@ __global__ void __launch_bounds__(64) k_post(const KArgs)
 {
     const int G = kargs().c.reset_slots, b = (int)blockIdx.x;
     if (b < G) {
-        autoreset_worker<MS, false, RO, true>(b, G);
+        extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+        autoreset_worker<MS, false, RO, true>(b, G, lds);
     } else {
         const KArgs &A = kargs();
         if constexpr (NPF == 0) encode_one(A.c, A.st, A.o, b - G);
@@ -2290,7 +2303,8 @@ __global__ void __launch_bounds__(64) k_post(const KArgs)
 // (cfg5's 40x40 x 4 frames: 1600 dwords): four waves share one LDS image, a
 // quarter of the LDS per wave, and 7 prefetched dwords per thread instead of 25.
 template <int NPW, int T>
-__global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_state st, const snake_out o)
+__device__ __forceinline__ void encode_lean_block(const KCfg &c, const snake_state &st, const snake_out &o,
+                                                  const int blk)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
@@ -2318,7 +2332,7 @@ __global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_sta
     }
     OBSMIN(1404, lane);
     zero_lean<T>(c, pf, lane);
-    const int e_begin = blockIdx.x * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
+    const int e_begin = blk * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
     uint32_t w[NPW];
     int pcur = 0, pctr = 0, pskip = 0;
 #define SNAKE_LEAN_FETCH(EE)                                                                       \
@@ -2350,6 +2364,33 @@ __global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_sta
     }
 #undef SNAKE_LEAN_FETCH
     OBSMAX(1403, lane);
+}
+
+template <int NPW, int T>
+__global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_state st, const snake_out o)
+{
+    encode_lean_block<NPW, T>(c, st, o, (int)blockIdx.x);
+}
+
+// The shared phase of a background-spawn-ahead board with four-wave lean
+// encodes (cfg5) as one launch (KCfg.post_lean): workgroups [0, ceil(reset_slots
+// / 4)) hold four independent resets-only workers each (wave w of workgroup b
+// is worker 4b + w, with its own KCfg.lds_worker bytes of LDS and, for a reset
+// that finds no ready record, its own global link table: no workgroup barrier
+// on their path), the rest are lean-encode workgroups. No side stream: the
+// fork's and the join's cross-stream latency (12 and 16 us at cfg5) go away.
+template <int MS>
+__global__ void __launch_bounds__(256) k_post_lean(const KArgs)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int G = kargs().c.reset_slots, GB = (G + 3) >> 2, b = (int)blockIdx.x;
+    if (b < GB) {
+        const int wave = (int)(threadIdx.x >> 6), wid = 4 * b + wave;
+        if (wid < G) autoreset_worker<MS, false, true, false>(wid, G, lds + wave * kargs().c.lds_worker);
+    } else {
+        const KArgs &A = kargs();
+        encode_lean_block<8, 256>(A.c, A.st, A.o, b - GB);
+    }
 }
 
 template <int MS, bool JL>
@@ -2750,6 +2791,25 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     };
     SideCtx sc;
     if ((rc = side_ctx(sm, dg.dev, &sc))) return rc;
+    if (k.post_lean && bgc && st.jscratch && k.lean && k.lean_threads == 256 && k.autoreset == 1) {
+        // one launch: four resets-only workers per workgroup, then the lean
+        // encodes (k_post_lean); the spawn kernel forks off after k_logic
+        if (hipEventRecord(sc.fork, sm) != hipSuccess) {
+            set_error("fork to the background stream failed");
+            return SNAKE_E_LAUNCH;
+        }
+        if ((rc = launch_spawn(sc.fork))) return rc;
+        const int epw2 = k.enc_per_wave;
+        const dim3 gp((k.reset_slots + 3) / 4 + (k.N + epw2 - 1) / epw2);
+        const int lds_p = std::max(4 * k.lds_worker, k.lds_lean_bytes);
+        const KArgs a{k, st, o, nullptr};
+        TimedLaunch t2("k_post", sm);
+        if (k.S <= 4) hipLaunchKernelGGL(k_post_lean<4>, gp, dim3(256), lds_p, sm, a);
+        else if (k.S <= 8) hipLaunchKernelGGL(k_post_lean<8>, gp, dim3(256), lds_p, sm, a);
+        else hipLaunchKernelGGL(k_post_lean<16>, gp, dim3(256), lds_p, sm, a);
+        t2.close();
+        return check_launch("k_post_lean");
+    }
     if (k.fused && !k.spawn_budget && k.link_in_lds && !k.lean) {
         // one launch on the caller's stream: workers, then encodes (k_post);
         // with background spawn-ahead the workers run the resets only (RO)

@@ -58,7 +58,10 @@ def test_plan_sizes(native):
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
     assert lay.obs_c == 32 and lay.obs == 8192 * 8 * 11 * 11 * 32
-    assert lay.n_cand == 16424 and lay.jscratch == 0              # u16 draw record fits LDS
+    # the u16 draw record fits LDS (the spawn kernel keeps it there), and with
+    # background spawn-ahead the one-launch workers (k_post_lean) keep a global
+    # link table per worker for resets without a ready record
+    assert lay.n_cand == 16424 and lay.jscratch == 2560 * (16424 + 64) * 4
     assert lay.spawn == 2 * 8192 * 656 * 4                        # background spawn-ahead: two records per env
     c = cfg(native, height=44, width=44, num_snakes=4)
     lay2 = native.SnakeLayout()
