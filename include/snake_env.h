@@ -182,9 +182,11 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
  * the same call and its out->obs holds the reset observation. Launches: k_logic
  * (the game rules of every env, queueing the auto-resets), then k_post on
  * `stream`, whose first blocks are the reset workers and the rest the encodes of
- * every other env's observation. With background spawn-ahead or a spawn time
- * slice the workers (k_autoreset) run on `stream` concurrently with k_encode on a
- * side stream the library keeps per caller stream, joined before the call
+ * every other env's observation (k_post_lean: four resets-only workers per
+ * workgroup, then four-wave lean encodes, for background spawn-ahead boards such
+ * as 40x40 with 4 frames). Elsewhere (a spawn time slice, other background
+ * boards) the workers (k_autoreset) run on `stream` concurrently with k_encode
+ * on a side stream the library keeps per caller stream, joined before the call
  * returns.
  *
  * Spawn-ahead: a reset's spawn poses depend only on the env's MT19937 state, which
