@@ -292,7 +292,8 @@ def main():
         # the shared phase as one launch (k_post: reset workers + encodes): its
         # bytes are the encodes', the resets' and the spawn-ahead attempts'
         rk, rk_ms = 'k_post', kern['k_post']
-        jobs_per_step = sp_jobs / n_timed if n_timed else 0.0
+        # (with background spawn-ahead the attempts are k_spawn's, not k_post's)
+        jobs_per_step = sp_jobs / n_timed if n_timed and kern['k_spawn'] == 0 else 0.0
         launch_bytes = (Be * encoded_per_launch
                         + reset_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
                         * resets / args.steps + spawn_bytes(S) * jobs_per_step)
