@@ -89,7 +89,7 @@ typedef struct {
     int64_t stats;      /* snake_epi_stat [N][S]         running episode score/steps/fruits/kills */
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
     int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
-    int64_t jscratch;   /* uint32 [min(N,2560)][round4(n_cand)+64] reset link tables, 0 when the
+    int64_t jscratch;   /* uint32 [min(N,2048)][round4(n_cand)+64] reset link tables, 0 when the
                                                          u16 draw record fits LDS (2*n_cand <= 36 KB)
                                                          and spawn-ahead is not in the background */
     int64_t spawn;      /* uint32 [N][656]               spawn-ahead record: MT key, MT pos and the

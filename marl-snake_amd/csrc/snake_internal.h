@@ -13,7 +13,7 @@ constexpr int kMaxSnakes = 16;
 constexpr int kMaxFruits = 64;
 constexpr int kEnvRec = 8;          // int32 words per env record
 constexpr int kJarrLdsMax = 36864;  // bytes of a reset's u16 draw record kept in LDS
-constexpr int kResetSlots = 2560;   // concurrent reset workers (global link tables); 2048: +2 % step time
+constexpr int kResetSlots = 2048;   // concurrent reset workers (global link tables): 8 per CU; with k_post 2 048 beat 2 560 (cfg3 0.0905 -> 0.0892 ms; 1 536 0.106)
 constexpr int kQShards = 64;        // auto-reset queue shards (k_logic block % 64)
 constexpr int kStageMax = 8192;     // bytes of staged observation per encode group
 constexpr int kSpawnStride = 656;   // u32 words per spawn-ahead record: key, pos, poses

@@ -61,12 +61,12 @@ def test_plan_sizes(native):
     # the u16 draw record fits LDS (the spawn kernel keeps it there), and with
     # background spawn-ahead the one-launch workers (k_post_lean) keep a global
     # link table per worker for resets without a ready record
-    assert lay.n_cand == 16424 and lay.jscratch == 2560 * (16424 + 64) * 4
+    assert lay.n_cand == 16424 and lay.jscratch == 2048 * (16424 + 64) * 4
     assert lay.spawn == 2 * 8192 * 656 * 4                        # background spawn-ahead: two records per env
     c = cfg(native, height=44, width=44, num_snakes=4)
     lay2 = native.SnakeLayout()
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay2)) == 0
-    assert lay2.n_cand == 20168 and lay2.jscratch == 2560 * (20168 + 64) * 4   # global link tables
+    assert lay2.n_cand == 20168 and lay2.jscratch == 2048 * (20168 + 64) * 4   # global link tables
     assert lay.grid == 8192 * 4 * 1600
     # paused spawn-ahead attempts: u16 per draw index per env where attempts are
     # sliced (an explicit spawn_budget_us; LDS draw record, spawn-ahead on),
