@@ -177,9 +177,10 @@ def main():
     ap.add_argument('--dump-dir', default=None,
                     help='write rank<r>.npz with the shard range, final grids, MT keys/positions, '
                          'env records, the last step\'s obs and each env\'s summed rewards')
-    ap.add_argument('--timing-stride', type=int, default=32,
+    ap.add_argument('--timing-stride', type=int, default=None,
                     help='bracket the kernels of every k-th timed step with timing events '
-                         '(0: none; a timed step costs ~25 us more: measured 0.1034 ms per step at stride 32 vs 0.1025 untimed, cfg3)')
+                         '(0: none; default max(1, min(32, steps // 4)), so at least 4 launches are '
+                         'averaged; a timed step costs ~1-2 us more: 0.1034 ms per step at stride 32 vs 0.1025 untimed, cfg3)')
     args = ap.parse_args()
     for k, v in PRESETS[args.config].items():
         if getattr(args, k) is None:
@@ -248,9 +249,10 @@ def main():
     torch.cuda.synchronize(device)
 
     L = _native.lib()
-    for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_post', 'k_spawn', 'resets', 'spawn_hits', 'spawn_jobs'):
+    for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_post', 'k_spawn', 'resets', 'resets_timed', 'spawn_hits',
+              'spawn_jobs'):
         _native.timing_read(k, L)                      # drop anything from the warmup
-    stride = args.timing_stride
+    stride = args.timing_stride if args.timing_stride is not None else max(1, min(32, args.steps // 4))
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -275,11 +277,15 @@ def main():
     for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_post', 'k_spawn'):
         ms, n = _native.timing_read(k, L)
         kern[k] = ms / max(n, 1)
-    resets = _native.timing_read('resets', L)[1]
-    # spawn-ahead counters (counted on the timed-event steps only)
+    resets = _native.timing_read('resets', L)[1]              # every timed step
+    # counted on the event-timed steps only, the steps the kernel times come from:
+    # the auto-resets, the resets served from a spawn-ahead record, the attempts
     n_timed = len(range(0, args.steps, stride)) if stride > 0 else 0
+    resets_t = _native.timing_read('resets_timed', L)[1]
     sp_hits = _native.timing_read('spawn_hits', L)[1]
     sp_jobs = _native.timing_read('spawn_jobs', L)[1]
+    # per launch on the event-timed steps (all steps when no step is timed)
+    rps_t = resets_t / n_timed if n_timed else resets / args.steps
 
     red = reduce_max([elapsed] + list(kern.values()), red_device, dist if distributed else None)
     elapsed, kern = red[0], dict(zip(kern, red[1:]))
@@ -287,7 +293,7 @@ def main():
     lay = venv.layout
     B = algorithmic_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
     Be = encode_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
-    encoded_per_launch = (hi - lo) - resets / args.steps
+    encoded_per_launch = (hi - lo) - rps_t
     if kern['k_post'] > 0:
         # the shared phase as one launch (k_post: reset workers + encodes): its
         # bytes are the encodes', the resets' and the spawn-ahead attempts'
@@ -296,7 +302,7 @@ def main():
         jobs_per_step = sp_jobs / n_timed if n_timed and kern['k_spawn'] == 0 else 0.0
         launch_bytes = (Be * encoded_per_launch
                         + reset_bytes(S, lay.obs_h, lay.obs_w, args.frame_stack, args.height, args.width)
-                        * resets / args.steps + spawn_bytes(S) * jobs_per_step)
+                        * rps_t + spawn_bytes(S) * jobs_per_step)
     else:
         rk, rk_ms = 'k_encode', kern['k_encode']
         launch_bytes = Be * encoded_per_launch
@@ -328,16 +334,22 @@ def main():
                    'snake_length': 3, 'parallelism': f'env-shard x{world}'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                     'traffic': None, 'kernel': rk, 'kernel_ms': round(rk_ms, 4),
+                     'traffic': None, 'kernel': rk, 'kernel_ms': round(rk_ms, 4), 'timed_launches': n_timed,
                      'algorithmic_bytes_per_launch': round(launch_bytes),
                      'bytes_per_encoded_env': Be},
         'step_roofline': {'achieved': round(step_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                           'frac': round(step_gbs / HBM_PEAK_GBS, 4), 'bytes_per_env_step': B},
         'kernels': {k: round(v, 4) for k, v in kern.items()},
         'resets_per_step': round(resets / args.steps, 1),
+        'resets_per_timed_step': round(rps_t, 1),
+        # every env is reset at once before the warmup; its episodes end ~20-120
+        # steps later, so a short warmup times that wave of resets, not the steady
+        # rate (~1 036 per step at cfg3 past ~200 steps)
+        'regime': ('steady (warmup >= 200 steps after env.reset())' if args.warmup >= 200 else
+                   f'post-reset transient (steps {args.warmup}-{args.warmup + args.steps} after env.reset())'),
         'spawn_ahead': ({'hits_per_step': round(sp_hits / n_timed, 1),
                          'jobs_per_step': round(sp_jobs / n_timed, 1),
-                         'hit_rate': round(sp_hits / n_timed / max(resets / args.steps, 1e-9), 4)}
+                         'hit_rate': round(sp_hits / max(resets_t, 1), 4)}
                         if n_timed else None),
         'cpu_baseline': None,
     }
@@ -345,6 +357,7 @@ def main():
     if args.dump_dir:
         import numpy as np
         os.makedirs(args.dump_dir, exist_ok=True)
+        venv.sync()   # (after the last background spawn kernel, which writes env word 4)
         keys, pos = venv.mt_state()
         np.savez(os.path.join(args.dump_dir, f'rank{rank}.npz'), lo=lo, hi=hi, world=world,
                  grids=venv.grids().cpu().numpy(), mt=keys.cpu().numpy(), mt_pos=pos.cpu().numpy(),

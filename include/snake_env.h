@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 13
+#define SNAKE_ABI_VERSION 14
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -53,22 +53,14 @@ typedef struct {
                                    2 = reset every env after every step (gym 0.23.1's
                                    worker behind make_snake, wrappers.py:212) */
     int32_t spawn_ahead;        /* spawn-ahead threshold (snake_step): 0 = default (at most
-                                   2 live snakes, every env under coop; the environment
-                                   variable SNAKE_SPAWN_THR overrides), -1 = off, k >= 1 =
+                                   2 live snakes, every env under coop), -1 = off, k >= 1 =
                                    envs with at most k live snakes. Never changes results. */
-    int32_t spawn_budget_us;    /* time slice of the spawn-ahead jobs per snake_step, in us
-                                   from the reset workers' start: an attempt still drawing at
-                                   the slice's end is paused (status 3, its draws kept in
-                                   st->spawn_draws) and continued by a later step, or finished
-                                   by the env's reset. 0 = automatic (unlimited;
-                                   SNAKE_SPAWN_BUDGET_US overrides), -1 = unlimited. Never
-                                   changes results. */
     int32_t spawn_background;   /* 1 = the spawn-ahead attempts run in a background kernel on a
                                    stream of the library's that outlives snake_step (see
-                                   snake_sync), 0 = automatic (on for boards of more than 8192
-                                   spawn poses, e.g. 40x40; SNAKE_BG overrides), -1 = off (inside
-                                   the step). Needs spawn-ahead on, unsliced attempts and the
-                                   draw record in LDS. Never changes results. */
+                                   snake_sync, snake_release), 0 = automatic (on for boards of
+                                   more than 8192 spawn poses, e.g. 40x40), -1 = off (inside the
+                                   step). Needs spawn-ahead on and a draw record that fits LDS
+                                   (at most 18 368 spawn poses). Never changes results. */
 } snake_cfg;
 
 /* Byte sizes of every caller-allocated buffer for num_envs envs (snake_plan). */
@@ -81,24 +73,23 @@ typedef struct {
     int64_t env;        /* int32  [N][8]                 alive_snakes, episode_length, cur, mt_pos
                                                          (> 624: the key's twist is pending, position
                                                          624 + j = word j of the next key),
-                                                         spawn-ahead status (bits 0-1: 0 none, 1 partial,
-                                                         2 ready, 3 an attempt in progress; bits 2-31: the
-                                                         record's generation),
-                                                         spawn failure (1: the last reset gave up, below) */
+                                                         spawn-ahead status word (bits 0-1: 0 none,
+                                                         1 partial, 2 ready; bit 2: which of the env's two
+                                                         records holds it (background spawn-ahead); bits
+                                                         3-31: the record's generation),
+                                                         spawn failure (1: the last reset gave up, below);
+                                                         words 6-7 unused */
     int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */
     int64_t stats;      /* snake_epi_stat [N][S]         running episode score/steps/fruits/kills */
     int64_t mt;         /* uint32 [N][624]               per-env MT19937 key */
     int64_t cand;       /* int16  [n_cand][L]            spawn-pose table (cell indices) */
     int64_t jscratch;   /* uint32 [min(N,2048)][round4(n_cand)+64] reset link tables, 0 when the
                                                          u16 draw record fits LDS (2*n_cand <= 36 KB)
-                                                         and spawn-ahead is not in the background */
+                                                         and the board's auto-resets do not run beside
+                                                         four-wave lean encodes (k_post_lean) */
     int64_t spawn;      /* uint32 [N][656]               spawn-ahead record: MT key, MT pos and the
                                                          S spawn-pose indices of the env's next reset
-                                                         (word 648: the next draw index of a paused
-                                                         attempt) */
-    int64_t spawn_draws;/* uint16 [N][round8(n_cand)]    draws of paused spawn-ahead attempts (j_i at
-                                                         index i); 0 when attempts are not sliced
-                                                         (spawn-ahead off, or global link tables) */
+                                                         ([2][N][656] with background spawn-ahead) */
     int64_t resetq;     /* int32  2 x ([3][64][cap] + [226*32]) sharded auto-reset and spawn-ahead
                                                          queues + the step's counters, one per 128-B
                                                          line; two sets, by step parity (zero-initialised) */
@@ -138,7 +129,6 @@ typedef struct {        /* device state buffers (layouts in snake_layout) */
     const int16_t *cand;
     uint32_t *jscratch; /* may be NULL when layout.jscratch == 0 */
     uint32_t *spawn;
-    uint16_t *spawn_draws; /* may be NULL when layout.spawn_draws == 0 (attempts then run whole) */
     int32_t  *resetq;   /* zero-initialised once by the caller */
 } snake_state;
 
@@ -180,15 +170,14 @@ int snake_reset(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
 
 /* SnakeEnv.step(actions) (snake_env.py:301-414) for all envs at once; actions is
  * int8 [N][S]. With cfg->autoreset an env whose dones are all True is reset in
- * the same call and its out->obs holds the reset observation. Launches: k_logic
- * (the game rules of every env, queueing the auto-resets), then k_post on
- * `stream`, whose first blocks are the reset workers and the rest the encodes of
- * every other env's observation (k_post_lean: four resets-only workers per
- * workgroup, then four-wave lean encodes, for background spawn-ahead boards such
- * as 40x40 with 4 frames). Elsewhere (a spawn time slice, other background
- * boards) the workers (k_autoreset) run on `stream` concurrently with k_encode
- * on a side stream the library keeps per caller stream, joined before the call
- * returns.
+ * the same call and its out->obs holds the reset observation. Launches, all on
+ * `stream`: k_logic (the game rules of every env, queueing the auto-resets),
+ * then k_post, whose first blocks are the reset workers and the rest the encodes
+ * of every other env's observation (k_post_lean: four workers per workgroup, then
+ * four-wave lean encodes, for boards with rings of 513-2048 dwords such as 40x40
+ * with 4 frames). Background spawn-ahead adds k_spawn on the library's stream
+ * for the state (snake_sync). Without autoreset: k_logic, k_encode; every-step
+ * autoreset: k_logic, k_autoreset, k_encode.
  *
  * Spawn-ahead: a reset's spawn poses depend only on the env's MT19937 state, which
  * changes only at fruit respawns and resets. With autoreset, k_logic also queues
@@ -213,6 +202,12 @@ int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,
  * `stream` wait for it (a no-op without background work). */
 int snake_sync(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, void *stream);
 
+/* Releases what the library keeps for this state (the background spawn-ahead
+ * stream and events, created by its first snake_step): waits for its last
+ * spawn kernel on the host, then destroys them. Call before freeing the state
+ * buffers; a later snake_step on the same buffers creates them afresh. */
+int snake_release(const snake_cfg *cfg, const snake_state *st, int64_t num_envs);
+
 /* RGB image of every env's current grid: rgb_from_grid(grid, Cell, CellColors)
  * (grid_util.py:164-175), the frame of SnakeEnv.render('rgb_array') and of the
  * 'gif' frames via image_from_grid (snake_env.py:284-293). palette is HOST
@@ -227,9 +222,10 @@ int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_en
  * is bracketed by timing events on its own stream. snake_timing_read returns the
  * summed device time (ms) and the launch count of one kernel ("k_logic",
  * "k_post", "k_autoreset", "k_encode", "k_spawn", "k_reset") since its last read, and the number of
- * auto-resets run (kernel "resets": count only); it waits for the events.
- * "spawn_hits" / "spawn_jobs" count (while enabled) the auto-resets that started
- * from a ready spawn-ahead record and the spawn-ahead attempts run. */
+ * auto-resets run (kernel "resets": count only, every step); it waits for the
+ * events. "resets_timed", "spawn_hits" and "spawn_jobs" count, while enabled,
+ * the auto-resets, those that started from a ready spawn-ahead record and the
+ * spawn-ahead attempts run. */
 int snake_timing_enable(int on);
 int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
 

@@ -246,51 +246,71 @@ static double disjoint_prob(int H, int W, int L, int S, int64_t *samples)
 // probability happens for fewer than ~2e-6 of the resets.
 constexpr double kMinDisjoint = 2e-4;
 
-// The spawn-ahead time slice in us (include/snake_env.h spawn_budget_us), > 0
-// when attempts are sliced. Automatic (0) = unlimited: slicing measured no gain
-// at 20x20 (cfg2/cfg3) and a loss at 40x40 (cfg5 step 0.1521 vs 0.1478 ms: the
-// paused attempts' resets and the sliced worker's register cost outweigh the
-// shorter tail); SNAKE_SPAWN_BUDGET_US overrides. N and enc_bytes are kept for
-// the A/B override's per-step scaling (0 < budget: as given).
-static int64_t spawn_budget_us(const snake_cfg *c, int64_t n_cand, int64_t N = 0, int64_t enc_bytes = 0)
-{
-    static const char *ev_bud = getenv("SNAKE_SPAWN_BUDGET_US");
-    (void)n_cand; (void)N; (void)enc_bytes;
-    int64_t us = c->spawn_budget_us;
-    if (us == 0) us = ev_bud ? atoll(ev_bud) : -1;
-    return us;
-}
-
 // spawn-ahead threshold: by default envs with at most 2 live snakes
 // (any env under coop, where one death ends the episode); -1 = off
 static int spawn_thr_of(const snake_cfg *c)
 {
-    static const char *ev = getenv("SNAKE_SPAWN_THR");
     int thr;
     if (c->spawn_ahead != 0) thr = c->spawn_ahead < 0 ? -1 : c->spawn_ahead;
-    else thr = ev ? atoi(ev) : (c->coop ? c->num_snakes : 2);
+    else thr = c->coop ? c->num_snakes : 2;
     if (c->autoreset != 1) thr = -1;   // (every-step resets: nothing to draw ahead)
     return thr;
 }
 
 // Background spawn-ahead (snake_kernels.hip k_spawn): the attempts leave the
 // step entirely (the step never waits for them; two steps later its k_logic
-// does, for the queue set). Needs spawn-ahead on (all-done auto-reset),
-// unsliced attempts and the draw record in LDS. cfg->spawn_background: 0
-// automatic (SNAKE_BG overrides), 1 on, -1 off. Automatic: boards of more than
-// 8192 spawn poses, whose attempt outlasts a step (40x40: ~110 us); at 20x20
-// the background jobs slowed the concurrent encodes more than they saved
-// (cfg3 0.111 -> 0.124 ms with the one-step wait).
+// does, for the queue set). Needs spawn-ahead on (all-done auto-reset) and the
+// draw record in LDS. cfg->spawn_background: 0 automatic, 1 on, -1 off.
+// Automatic: boards of more than 8192 spawn poses, whose attempt outlasts a
+// step (40x40: ~110 us); at 20x20 the background jobs slowed the concurrent
+// encodes more than they saved (cfg3 0.111 -> 0.124 ms with the one-step wait).
 static bool bg_of(const snake_cfg *c, int64_t n_cand)
 {
-    static const char *ev_bg = getenv("SNAKE_BG");
-#ifndef SNAKE_BG_DEFAULT
-#define SNAKE_BG_DEFAULT 1
-#endif
-    const bool want = c->spawn_background != 0 ? c->spawn_background > 0
-                                                : (ev_bg ? atoi(ev_bg) != 0 : (SNAKE_BG_DEFAULT && n_cand > 8192));
-    return want && spawn_thr_of(c) >= 0 && spawn_budget_us(c, n_cand) <= 0 &&
-           2 * (n_cand + kWave) <= kJarrLdsMax;
+    const bool want = c->spawn_background != 0 ? c->spawn_background > 0 : n_cand > 8192;
+    return want && spawn_thr_of(c) >= 0 && 2 * (n_cand + kWave) <= kJarrLdsMax;
+}
+
+// Lean-encode geometry (snake_kernels.hip encode_lean): the frames copied into a
+// zero-bordered LDS image (lp columns / vr rows of padding, pw bytes per row,
+// pframe bytes per frame) so the crop needs no bounds test; unit -> (snake, row,
+// col, frame) by multiply-high reciprocals of ups = oh*ow*fs, rowl = ow*fs, fs,
+// and of W/4. Used (lean = 1) for rings of 513 to 2 048 dwords, W % 4 == 0, when
+// every reciprocal is exact: four-wave workgroups (cfg5 k_encode 91 -> 66 us);
+// one wave per env measured slower beside the reset workers at one frame (cfg3
+// step 0.1216 vs 0.1032 ms), so smaller rings keep the staged encode.
+struct LeanGeom {
+    int lean, lp, pw, pframe, lds_lean_bytes, ups, rowl;
+    uint32_t mag_ups, mag_rowl, mag_fs, mag_wpr;
+};
+
+static LeanGeom lean_geom(const snake_cfg *c)
+{
+    LeanGeom g;
+    const int vr = c->vision_range, fs = c->frame_stack, H = c->height, W = c->width, S = c->num_snakes;
+    const int oh = vr ? 2 * vr + 1 : H, ow = vr ? 2 * vr + 1 : W;
+    const int64_t units = (int64_t)S * oh * ow * fs;
+    g.lp = vr ? (int)round_up(vr, 4) : 0;
+    g.pw = vr ? (int)round_up(W + g.lp + vr, 4) : W;
+    g.pframe = (int)round_up((int64_t)(H + 2 * vr) * g.pw, 16);
+    g.ups = oh * ow * fs;
+    g.rowl = ow * fs;
+    auto mag = [](uint64_t d) { return (uint32_t)(((1ull << 32) + d - 1) / d); };
+    g.mag_ups = mag(g.ups); g.mag_rowl = mag(g.rowl); g.mag_fs = mag(fs);
+    g.mag_wpr = mag(std::max(1, W / 4));
+    g.lds_lean_bytes = (int)round_up((int64_t)fs * g.pframe, 16) + 4 * fs * kMaxSnakes;
+    const int64_t fdw = (int64_t)fs * H * W / 4;
+    bool ok = fdw > 8 * kWave && fdw <= 8 * 256 && (units % 2) == 0 && units < (1 << 22) &&
+              g.lds_lean_bytes <= 48 * 1024 && W % 4 == 0;
+    for (int64_t u = 0; ok && u < units; u++) {
+        const int64_t q = ((uint64_t)u * g.mag_ups) >> 32, r0 = u - q * g.ups;
+        const int64_t i = ((uint64_t)r0 * g.mag_rowl) >> 32, r1 = r0 - i * g.rowl;
+        const int64_t j = fs == 1 ? r1 : ((uint64_t)r1 * g.mag_fs) >> 32;   // (snake_kernels.hip fdiv)
+        ok = q == u / g.ups && i == r0 / g.rowl && j == r1 / fs;
+    }
+    for (int64_t x = 0; ok && x < (int64_t)H * W / 4; x++)
+        ok = (W / 4 == 1 ? x : (int64_t)(((uint64_t)x * g.mag_wpr) >> 32)) == x / (W / 4);
+    g.lean = ok ? 1 : 0;
+    return g;
 }
 
 // Queue entries per shard: k_logic's blocks of E envs spread over kQShards
@@ -330,19 +350,13 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     // perm_trace): the u16 draw record in LDS up to kJarrLdsMax bytes, else one
     // global u32 link table per reset worker.
     const int64_t link = (round_up(o->n_cand, 4) + kWave) * 4;
-    // (background spawn-ahead boards too: k_post_lean's workers keep no draw
-    // record in LDS, a reset without a ready record uses its link table)
-    o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax && !bg_of(c, o->n_cand))
+    // (also the four-wave lean-encode boards' auto-resets: k_post_lean's workers
+    // keep no draw record in LDS)
+    const bool lean_workers = c->autoreset == 1 && lean_geom(c).lean;
+    o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax && !lean_workers)
                       ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     // (background spawn-ahead: two records per env, see k_spawn)
     o->spawn = (bg_of(c, o->n_cand) ? 2 : 1) * N * kSpawnStride * 4;
-    // paused spawn-ahead attempts keep their draws here (u16 per draw index):
-    // only where attempts are sliced (spawn_budget_us) -- spawn-ahead on
-    // (all-done auto-reset), the draw record in LDS -- and below 32 GiB
-    if (c->autoreset == 1 && c->spawn_ahead != -1 && o->jscratch == 0 && spawn_budget_us(c, o->n_cand) > 0) {
-        const int64_t bytes = N * round_up(o->n_cand, 8) * 2;
-        o->spawn_draws = bytes <= ((int64_t)32 << 30) ? bytes : 0;
-    }
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
         // kQShards) with room for every env of its blocks, + the step's counters
         // (kQCount, each in its own line); sized for any k_logic lane grouping
@@ -433,136 +447,45 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // the LDS draw record: u16 per index < n_cand + one dummy slot per lane
     const int jbytes = (int)round_up(2 * ((int64_t)k->n_cand + kWave), 16);
     k->link_in_lds = jbytes <= kJarrLdsMax;
-    // tuning knobs (A/B probes): workers of k_autoreset (<= kResetSlots, the
-    // global link tables are sized for that) and the spawn-ahead wave priority
-    static const char *ev_slots = getenv("SNAKE_RESET_SLOTS");
-    static const char *ev_prio = getenv("SNAKE_SPAWN_PRIO");
-    const int slots = ev_slots ? std::max(1, std::min(kResetSlots, atoi(ev_slots))) : kResetSlots;
-    k->reset_slots = (int)std::min<int64_t>(N, slots);
+    // reset workers (<= kResetSlots, the global link tables are sized for that)
+    k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
+    const bool bg = bg_of(c, n_cand);
     // spawn-ahead jobs at 1, below the encodes; small batches with in-step
     // spawn-ahead at 3 (a lone attempt is there the step's critical path: cfg2
     // 0.0510 -> 0.0494 ms; at cfg3 it costs 0.0905 -> 0.0960)
-    k->spawn_prio = ev_prio ? std::max(0, std::min(3, atoi(ev_prio))) : (N <= 8192 && !bg_of(c, n_cand) ? 3 : 1);
-    // k_encode above the spawn-ahead jobs: the bandwidth-bound encodes then keep
-    // HBM busy while the compute-bound workers fill the issue gaps (SNAKE_ENCODE_PRIO,
-    // default 2: step 0.1275 -> 0.1200 ms at cfg3; 0 = hardware default). With
-    // background spawn-ahead (set below) the step's resets are the critical path
-    // beside the encodes instead: default 0 (cfg5 0.160 -> 0.135 ms).
-    static const char *ev_eprio = getenv("SNAKE_ENCODE_PRIO");
-    k->encode_prio = ev_eprio ? std::max(0, std::min(3, atoi(ev_eprio))) : (bg_of(c, n_cand) ? 0 : 2);
-    // SNAKE_SPAWN_CAP=1: the other (2-live-snake) spawn-ahead jobs past the
-    // workers' first round wait for a later step (the urgent ones never do);
-    // off by default: measured 0.121 vs 0.109 ms at cfg3 (the hit rate falls)
-    static const char *ev_cap = getenv("SNAKE_SPAWN_CAP");
-    k->spawn_cap = ev_cap ? (atoi(ev_cap) != 0) : 0;
-    static const char *ev_redo = getenv("SNAKE_SPAWN_REDO");
-#ifndef SNAKE_SPAWN_REDO_DEFAULT
-#define SNAKE_SPAWN_REDO_DEFAULT 0
-#endif
-    k->spawn_redo = ev_redo ? (atoi(ev_redo) != 0) : SNAKE_SPAWN_REDO_DEFAULT;
+    k->spawn_prio = N <= 8192 && !bg ? 3 : 1;
+    // the encodes above the spawn-ahead jobs: the bandwidth-bound encodes then
+    // keep HBM busy while the compute-bound workers fill the issue gaps (cfg3
+    // 0.1275 -> 0.1200 ms against the hardware default 0). With background
+    // spawn-ahead the step's resets are the critical path beside the encodes
+    // instead: 0 (cfg5 0.160 -> 0.135 ms).
+    k->encode_prio = bg ? 0 : 2;
     {
         // k_logic's lanes per env (4, 8 or 16 >= S; 64 / that = envs per wave):
         // the fewest lanes that hold S snakes; small batches at least 8 (more,
         // shorter waves: cfg2's 4 096 envs k_logic 16.4 -> 15.3 us, step 0.0540
-        // -> 0.0527 ms; 16 lanes 18.0 us; at cfg3 8 lanes cost 6 us). SNAKE_LOGIC_MS
-        // overrides.
+        // -> 0.0527 ms; 16 lanes 18.0 us; at cfg3 8 lanes cost 6 us)
         const int ms_min = k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16);
-        static const char *ev_ms = getenv("SNAKE_LOGIC_MS");
-        const int ms = ev_ms ? atoi(ev_ms) : (N <= 8192 ? 8 : 0);
-        k->logic_ms = (ms == 4 || ms == 8 || ms == 16) && ms >= ms_min ? ms : ms_min;
+        k->logic_ms = N <= 8192 ? std::max(ms_min, 8) : ms_min;
     }
     k->q_envs_per_block = kWave / k->logic_ms;
     k->q_cap = (int)queue_cap(N, k->q_envs_per_block);
     k->spawn_thr = spawn_thr_of(c);
-    // spawn-ahead time slice (spawn_budget_us above)
-    k->draws_stride = lay.spawn_draws ? (int)round_up(lay.n_cand, 8) : 0;
-    {
-        const int64_t enc = (int64_t)k->S * k->oh * k->ow * 8 * k->fs + (int64_t)k->fs * k->HW;
-        const int64_t us = spawn_budget_us(c, lay.n_cand, N, enc);
-#ifndef SNAKE_SLICE
-#define SNAKE_SLICE 1   // (0: whole attempts, for A/B builds)
-#endif
-        k->spawn_budget = (SNAKE_SLICE && us > 0 && k->draws_stride > 0 && k->spawn_thr >= 0)
-                              ? (int)std::min<int64_t>(us * 100, 1 << 30) : 0;
-    }
-    {   // background spawn-ahead (bg_of above)
-        k->bg = bg_of(c, lay.n_cand) && k->spawn_budget == 0 ? 1 : 0;
-        // the shared phase as one launch (k_post) where it applies: in-step
-        // spawn-ahead, the LDS draw record, the staged encodes
-        // (cfg3 0.0970 -> 0.0941 ms per step, cfg2 0.0591 -> 0.0539, same box)
-        static const char *ev_r1 = getenv("SNAKE_ROWS1");
-        k->rows1 = ev_r1 ? atoi(ev_r1) : 0;
-        // background spawn-ahead with four-wave lean encodes as one launch
-        // (k_post_lean; cfg5 0.1227 -> 0.1169 ms, same box)
-        static const char *ev_pl = getenv("SNAKE_POST_LEAN");
-        k->post_lean = ev_pl ? atoi(ev_pl) : 1;
-        static const char *ev_fu = getenv("SNAKE_FUSED");
-        k->fused = ev_fu ? atoi(ev_fu) : 1;
-        if (bg_of(c, lay.n_cand) != (k->bg != 0)) {
-            set_error("background spawn-ahead needs unsliced attempts");
-            return SNAKE_E_CONFIG;
-        }
-        static const char *ev_ss = getenv("SNAKE_SPAWN_SLOTS");
-        const int ss = ev_ss ? std::max(1, atoi(ev_ss)) : kResetSlots;
-        k->spawn_slots = (int)std::min<int64_t>(N, ss);
-        static const char *ev_bt = getenv("SNAKE_BG_TRIES");
-        k->bg_tries = ev_bt ? std::max(1, atoi(ev_bt)) : 1;
-    }
+    k->bg = bg ? 1 : 0;
+    k->spawn_slots = (int)std::min<int64_t>(N, kResetSlots);   // k_spawn workers
+    k->bg_tries = 1;   // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
     k->lds_obs_bytes = off;
-    {   // lean encode (snake_kernels.hip encode_lean): zero-bordered frames in LDS
-        static const char *ev_lean = getenv("SNAKE_LEAN");
-#ifndef SNAKE_LEAN_DEFAULT
-#define SNAKE_LEAN_DEFAULT 1
-#endif
-        const bool want = ev_lean ? atoi(ev_lean) != 0 : SNAKE_LEAN_DEFAULT;
-        k->lp = k->vr ? (int)round_up(k->vr, 4) : 0;
-        k->pw = k->vr ? (int)round_up(k->W + k->lp + k->vr, 4) : k->W;
-        const int ph = k->H + 2 * k->vr;
-        k->pframe = (int)round_up((int64_t)ph * k->pw, 16);
-        k->ups = k->oh * k->ow * k->fs;
-        k->rowl = k->ow * k->fs;
-        auto mag = [](uint64_t d) { return (uint32_t)(((1ull << 32) + d - 1) / d); };
-        k->mag_ups = mag(k->ups); k->mag_rowl = mag(k->rowl); k->mag_fs = mag(k->fs);
-        k->mag_wpr = mag(std::max(1, k->W / 4));
-        k->lds_lean_bytes = (int)round_up((int64_t)k->fs * k->pframe, 16) + 4 * k->fs * kMaxSnakes;
-        // the reciprocals must be exact for every unit index and grid word
-        // (k_encode_lean: grids with W % 4 == 0, at most 8 prefetched frame dwords
-        // per thread: one wave per env up to 512 dwords, four up to 2048)
-        static const char *ev_lt = getenv("SNAKE_LEAN_THREADS");
-        const int64_t fdw = (int64_t)k->fs * k->HW / 4;
-        k->lean_threads = fdw <= 8 * kWave ? kWave : 256;
-        if (ev_lt && atoi(ev_lt) == 256) k->lean_threads = 256;
-        bool exact = (k->units % 2) == 0 && k->units < (1 << 22) && k->lds_lean_bytes <= 48 * 1024 &&
-                     k->W % 4 == 0 && fdw <= 8 * k->lean_threads;
-        for (int64_t u = 0; exact && u < k->units; u++) {
-            const int64_t q = ((uint64_t)u * k->mag_ups) >> 32, r0 = u - q * k->ups;
-            const int64_t i = ((uint64_t)r0 * k->mag_rowl) >> 32, r1 = r0 - i * k->rowl;
-            const int64_t j = k->fs == 1 ? r1 : ((uint64_t)r1 * k->mag_fs) >> 32;   // (snake_kernels.hip fdiv)
-            exact = q == u / k->ups && i == r0 / k->rowl && j == r1 / k->fs;
-        }
-        if (k->W % 4 == 0)
-            for (int64_t x = 0; exact && x < (int64_t)k->HW / 4; x++)
-                exact = (k->W / 4 == 1 ? x : (int64_t)(((uint64_t)x * k->mag_wpr) >> 32)) == x / (k->W / 4);
-        // default: only the four-wave form (rings over 512 dwords: cfg5 k_encode 91 ->
-        // 66 us); one wave per env measured slower beside the reset workers (cfg3
-        // step 0.1216 vs 0.1032 ms, cfg2 0.0639 vs 0.0621; SNAKE_LEAN=1 forces it)
-        k->lean = exact && (ev_lean ? want : (want && k->lean_threads == 256)) ? 1 : 0;
-    }
-    // envs per encode wave (k_encode_multi: the next env's ring prefetched into
-    // registers, at most 8 16-byte chunks per lane); SNAKE_ENC_PER_WAVE overrides
     {
-        static const char *ev_epw = getenv("SNAKE_ENC_PER_WAVE");
-#ifndef SNAKE_EPW_DEFAULT
-#define SNAKE_EPW_DEFAULT 2
-#endif
-        // (measured: 2 with the lean encode at cfg3/cfg2; one env per wave otherwise)
-        // (k_encode_multi, two envs per wave, for large batches: cfg3 step 0.1033 ->
-        // 0.0998 ms; cfg2's 4096 envs keep one per wave, 0.0622 vs 0.0625)
-        int epw = ev_epw ? atoi(ev_epw)
-                         : (k->lean ? (k->lean_threads == kWave ? SNAKE_EPW_DEFAULT : 2) : (N >= 16384 ? 2 : 1));
-        if (k->ring_bytes > 8 * 1024 && !k->lean) epw = 1;
-        k->enc_per_wave = std::max(1, std::min(epw, 64));
+        const LeanGeom g = lean_geom(c);
+        k->lean = g.lean; k->lp = g.lp; k->pw = g.pw; k->pframe = g.pframe;
+        k->lds_lean_bytes = g.lds_lean_bytes; k->ups = g.ups; k->rowl = g.rowl;
+        k->mag_ups = g.mag_ups; k->mag_rowl = g.mag_rowl; k->mag_fs = g.mag_fs; k->mag_wpr = g.mag_wpr;
     }
+    // envs per encode wave (k_post's encodes: the next env's ring prefetched into
+    // registers, at most 8 16-byte chunks per lane): two at 16 384 envs and more
+    // (cfg3 0.1033 -> 0.0998 ms; 4, 8, 16, 32 measured 0.1016, 0.106, 0.114,
+    // 0.135), one below (cfg2 0.0622 vs 0.0625); the lean encode two per workgroup
+    k->enc_per_wave = k->lean ? 2 : (N >= 16384 && k->ring_bytes <= 8 * 1024 ? 2 : 1);
     // the reset workers never use the encode staging buffer: the draw record
     // overlays it (the workers' LDS is what k_encode's waves share the CUs with)
     k->lds_link = k->lds_stage;
@@ -587,12 +510,8 @@ static int check_state(const KCfg &k, const snake_state *st, bool need_all)
         set_error("snake_state.resetq / spawn is NULL");
         return SNAKE_E_ARG;
     }
-    if (!k.link_in_lds && !st->jscratch) {
+    if ((!k.link_in_lds || (k.lean && k.autoreset == 1)) && !st->jscratch) {
         set_error("snake_state.jscratch is required for this config (n_cand=%d)", k.n_cand);
-        return SNAKE_E_ARG;
-    }
-    if (k.spawn_budget && !st->spawn_draws) {
-        set_error("snake_state.spawn_draws is required for this config (layout.spawn_draws > 0)");
         return SNAKE_E_ARG;
     }
     (void)need_all;
@@ -721,6 +640,15 @@ int snake_step(const snake_cfg *cfg, const snake_state *st, int64_t num_envs, co
     if ((rc = check_out(out, true))) return rc;
     if (!actions) { set_error("actions is NULL"); return SNAKE_E_ARG; }
     return launch_step(k, *st, actions, *out, stream);
+}
+
+int snake_release(const snake_cfg *cfg, const snake_state *st, int64_t num_envs)
+{
+    KCfg k;
+    int rc = plan_cached(cfg, num_envs, &k);
+    if (rc) return rc;
+    if (!st || !st->env) { set_error("snake_state.env is NULL"); return SNAKE_E_ARG; }
+    return release_background(*st);
 }
 
 int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_envs,

@@ -19,14 +19,10 @@ constexpr int kStageMax = 8192;     // bytes of staged observation per encode gr
 constexpr int kSpawnStride = 656;   // u32 words per spawn-ahead record: key, pos, poses
 constexpr int kSpawnPos = 624;      // record word: MT position after the recorded attempts
 constexpr int kSpawnSel = 625;      // record words [625, 625 + S): spawn-pose indices
-constexpr int kSpawnI = 648;        // record word: next draw index of a paused attempt (status INPROG)
 // Queue counters (zero between steps). Every counter sits in a line of its own
 // (kQSpread words apart): same-line device-scope atomics from thousands of
 // waves serialise at the memory side.
-#ifndef SNAKE_QSPREAD
-#define SNAKE_QSPREAD 32
-#endif
-constexpr int kQSpread = SNAKE_QSPREAD;
+constexpr int kQSpread = 32;
 constexpr int kClaimShards = 16;    // claim counters: worker w claims on shard w % 16
 constexpr int kNumQ = 3;            // queues: 0 resets, 1 urgent spawn-ahead (<= 1 live snake), 2 other spawn-ahead
 constexpr int kQClaim = kNumQ * kQShards;             // counter index of claim shard 0
@@ -41,11 +37,12 @@ constexpr int kQCounters = kQCount * kQSpread;        // words
 constexpr int kQSets = 2;
 constexpr int kQGenBits = 6;        // spawn queue entry (background mode): env | generation << 26
 
-// env record words
-enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, ENV_FAIL = 5, ENV_VOID = 6 };
-// spawn-ahead status (env word ENV_SPAWN bits 0-1; bits 2-31: the record's
-// generation, bumped by every k_logic draw that voids it)
-enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2, SPAWN_INPROG = 3 };
+// env record words (6, 7 unused)
+enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, ENV_FAIL = 5 };
+// spawn-ahead status word (env word ENV_SPAWN): bits 0-1 the status, bit 2 the
+// record buffer holding the record (background spawn-ahead keeps two per env),
+// bits 3-31 the record's generation (bumped by every MT draw that voids it)
+enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2 };
 
 // Everything a kernel needs, by value (a kernel argument).
 struct KCfg {
@@ -68,7 +65,6 @@ struct KCfg {
     // staged group (0: direct encode), the buffer, and magic reciprocals of
     // fs*oh and oh (x / d == umulhi(x, m) for the row indices used)
     int enc_group, lds_stage;
-    int rows1;                  // one-frame stacks: encode_rows1 (dword row reads, whole-cell stores)
     uint32_t mag_fsoh, mag_oh;
     uint32_t mag_W;             // x / W == umulhi(x, mag_W) for cell indices x < H*W
     uint32_t mag_n16;           // q / (grid_stride/16) == umulhi(q, mag_n16) for q < 2^32/n16
@@ -79,17 +75,10 @@ struct KCfg {
     int spawn_thr;              // queue spawn-ahead when <= this many snakes live (-1: off)
     int spawn_prio;             // wave priority of the spawn-ahead jobs (resets: 3)
     int encode_prio;            // wave priority of k_encode (beside the reset workers)
-    int spawn_cap;              // 1: other spawn-ahead jobs only in the workers' first round
-    int spawn_redo;             // 1: after a fruit draw voided its record, an env is queued again only
-                                //    once at most one snake lives (ENV_VOID marks the void)
-    int diag;                   // count spawn-ahead hits/jobs (while timing is enabled)
-    int spawn_budget;           // spawn-ahead time slice per step, s_memrealtime ticks (100 MHz); 0 = none
-    int draws_stride;           // u16 entries per env in st.spawn_draws (0: attempts are not sliced)
-    int enc_per_wave;           // envs per k_encode wave (1: k_encode, else k_encode_multi with prefetch)
-    int bg;                     // 1: spawn-ahead jobs in the background kernel k_spawn (not k_autoreset)
-    int fused;                  // 1: reset workers and encodes in one launch (k_post), no side stream
-    int post_lean;              // 1: background spawn-ahead + four-wave lean encodes in one launch (k_post_lean)
-    int lds_worker;             // k_post_lean: LDS bytes of one resets-only worker (no draw record)
+    int diag;                   // count spawn-ahead hits/jobs and resets (while timing is enabled)
+    int enc_per_wave;           // envs per encode wave of k_post (1: encode_one, else encode_multi with prefetch)
+    int bg;                     // 1: spawn-ahead jobs in the background kernel k_spawn (not in the step)
+    int lds_worker;             // k_post_lean: LDS bytes of one worker (no draw record)
     int qpar;                   // queue set of this step (0 unless bg)
     int spawn_slots;            // k_spawn workers
     int bg_tries;               // k_spawn: permutation attempts per job (until disjoint)
@@ -98,7 +87,6 @@ struct KCfg {
     // so the crop needs no bounds test; unit -> (snake, row, col, frame) by
     // multiply-high reciprocals of ups = oh*ow*fs, rowl = ow*fs, fs, and of W/4
     int lean, lp, pw, pframe, lds_lean_bytes, ups, rowl;
-    int lean_threads;           // threads per lean-encode workgroup (64, or 256 for rings over 512 dwords)
     uint32_t mag_ups, mag_rowl, mag_fs, mag_wpr;
     double rf, rk, rl, rw, rt, max_steps;
 };
@@ -115,6 +103,7 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
 int launch_step(const KCfg &k, const snake_state &st, const int8_t *actions, const snake_out &o,
                 void *stream);
 int wait_background(const snake_state &st, void *stream);
+int release_background(const snake_state &st);
 int launch_render(const KCfg &k, const snake_state &st, const uint8_t *palette, uint8_t *rgb,
                   void *stream);
 

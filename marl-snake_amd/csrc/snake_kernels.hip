@@ -31,17 +31,12 @@
 
 #include "snake_internal.h"
 
-#ifndef SNAKE_RESET_WAVES_PER_EU
-#define SNAKE_RESET_WAVES_PER_EU 4   // reset workers: 128 VGPRs (3 waves/SIMD measured slower)
-#endif
-
-#ifndef SNAKE_STEP_MIN_WAVES
-#define SNAKE_STEP_MIN_WAVES 1   // waves per SIMD the step kernel is register-budgeted for
-#endif
+constexpr int kResetWavesPerEU = 4;   // reset workers: 128 VGPRs (3 waves/SIMD measured slower)
 
 namespace snake {
 
-__device__ unsigned long long g_resets_run;   // auto-resets run (snake_timing_read "resets")
+__device__ unsigned long long g_resets_run;     // auto-resets run (snake_timing_read "resets")
+__device__ unsigned long long g_resets_timed;   // the same, while timing is enabled ("resets_timed")
 // (diagnostic counters, spread over 64 lines by block: one address taking a
 // device-scope atomic per job serialised thousands of them on the timed steps)
 constexpr int kDiagSlots = 64, kDiagSpread = 16;
@@ -50,36 +45,12 @@ __device__ unsigned long long g_spawn_jobs[kDiagSlots * kDiagSpread];   // spawn
 #define DIAG_ADD(arr) atomicAdd(&(arr)[(blockIdx.x % kDiagSlots) * kDiagSpread], 1ull)
 
 #ifdef SNAKE_STAMPS
-// Diagnostic build only: s_memtime stamps of env 0's wave at phase boundaries.
+// Diagnostic build only (scripts/logic_stamps.py): s_memtime stamps of block
+// 0's wave at k_logic's phase boundaries, and s_memrealtime (100 MHz) at every
+// k_logic wave's start and end (its block index, up to kWaveTimes blocks).
+constexpr int kWaveTimes = 8192;
 __device__ unsigned long long g_stamps[64];
-__device__ unsigned long long g_counts[8];
-__device__ unsigned long long g_obsprof[1408];  // realtime (100 MHz) of auto-resets / encodes / spawn jobs,
-                                                // then 5 words per auto-reset: 4 phase ends + spawn status
-#define OBSPROF(slot, lane)                                                          \
-    do { if ((lane) == 0) g_obsprof[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define OBSMAX(slot, lane)                                                           \
-    do { if ((lane) == 0) atomicMax(&g_obsprof[slot], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
-#define OBSMIN(slot, lane)                                                           \
-    do { if ((lane) == 0) atomicMax(&g_obsprof[slot], ~(unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
-#define RPROF(ps, p, lane)                                                           \
-    do { if ((ps) >= 0 && (lane) == 0) g_obsprof[768 + 5 * (ps) + (p)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define RPROF_VAL(ps, p, v, lane)                                                    \
-    do { if ((ps) >= 0 && (lane) == 0) g_obsprof[768 + 5 * (ps) + (p)] = (v); } while (0)
-#define STAMP(e, lane, idx)                                                        \
-    do {                                                                           \
-        if ((e) == 0) {                                                            \
-            __builtin_amdgcn_sched_barrier(0);                                     \
-            unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
-            if ((lane) == 0) g_stamps[idx] = _t;                                   \
-            __builtin_amdgcn_sched_barrier(0);                                     \
-        }                                                                          \
-    } while (0)
-#define COUNT(e, lane, idx) do { cnt_[idx]++; } while (0)
-#define COUNT_DECL unsigned long long cnt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
-#define COUNT_ADD(idx, v) do { cnt_[idx] += (v); } while (0)
-#define COUNT_FLUSH(e, lane)                                                       \
-    do { if ((e) == 0 && (lane) == 0) { for (int q_ = 0; q_ < 8; q_++) g_counts[q_] += cnt_[q_]; } } while (0)
-#define NOW() __builtin_amdgcn_s_memtime()
+__device__ unsigned long long g_wavetime[2 * kWaveTimes];
 #define LSTAMP(idx)                                                                \
     do {                                                                           \
         if (blockIdx.x == 0) {                                                     \
@@ -89,25 +60,16 @@ __device__ unsigned long long g_obsprof[1408];  // realtime (100 MHz) of auto-re
             __builtin_amdgcn_sched_barrier(0);                                     \
         }                                                                          \
     } while (0)
-#ifdef SNAKE_STAMPS_ROUNDS
-#define RNOW() __builtin_amdgcn_s_memtime()
+#define WTIME(end)                                                                 \
+    do {                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+        if (threadIdx.x == 0 && blockIdx.x < kWaveTimes)                           \
+            g_wavetime[2 * blockIdx.x + (end)] = __builtin_amdgcn_s_memrealtime(); \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+    } while (0)
 #else
-#define RNOW() 0ull
-#endif
-#else
-#define STAMP(e, lane, idx) do {} while (0)
-#define COUNT(e, lane, idx) do {} while (0)
-#define COUNT_DECL do {} while (0)
-#define COUNT_ADD(idx, v) do { (void)(v); } while (0)
-#define COUNT_FLUSH(e, lane) do {} while (0)
-#define NOW() 0ull
 #define LSTAMP(idx) do {} while (0)
-#define RNOW() 0ull
-#define OBSPROF(slot, lane) do {} while (0)
-#define OBSMAX(slot, lane) do {} while (0)
-#define OBSMIN(slot, lane) do {} while (0)
-#define RPROF(ps, p, lane) do {} while (0)
-#define RPROF_VAL(ps, p, v, lane) do { (void)(v); } while (0)
+#define WTIME(end) do {} while (0)
 #endif
 
 enum { C_EMPTY = 0, C_WALL = 1, C_FRUIT = 2, C_HEAD = 3, C_BODY = 4, C_TAIL = 5 };
@@ -199,6 +161,59 @@ __device__ __forceinline__ int wave_scan(int v, int lane)
 
 __device__ __forceinline__ int bcast(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
+// ---- exchanges inside k_logic's env groups of G = 4, 8 or 16 lanes (aligned
+// inside a 16-lane DPP row) by DPP moves, not through the LDS: a __shfl
+// (ds_bpermute) is an LDS round trip on the rules' dependency chain.
+// gsel<G, J>(v): the value of lane J of this lane's group.
+template <int G, int J>
+__device__ __forceinline__ int gsel(int v)
+{
+    static_assert(G == 4 || G == 8 || G == 16, "group of 4, 8 or 16 lanes");
+    if constexpr (G == 4) {
+        return __builtin_amdgcn_mov_dpp(v, J * 0x55, 0xf, 0xf, false);   // quad_perm:[J,J,J,J]
+    } else if constexpr (G == 16) {
+        return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, false);   // row_newbcast:J
+    } else {
+        // lane J & 3 of the lane's quad, then, in the group's other quad, that
+        // value moved over by four lanes
+        const int t = __builtin_amdgcn_mov_dpp(v, (J & 3) * 0x55, 0xf, 0xf, false);
+        const bool upper = (threadIdx.x & 4) != 0;
+        if constexpr (J < 4) return upper ? __builtin_amdgcn_mov_dpp(t, 0x114, 0xf, 0xf, false) : t;   // row_shr:4
+        else return upper ? t : __builtin_amdgcn_mov_dpp(t, 0x104, 0xf, 0xf, false);                   // row_shl:4
+    }
+}
+
+template <int G, int J>
+__device__ __forceinline__ double gsel(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = gsel<G, J>((int)b), hi = gsel<G, J>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (uint32_t)lo);
+}
+
+// inclusive prefix sum over the group (k = the lane's index in it)
+template <int G>
+__device__ __forceinline__ int gscan(int v, int k)
+{
+    v += k >= 1 ? __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false) : 0;   // row_shr:1
+    v += k >= 2 ? __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false) : 0;   // row_shr:2
+    if constexpr (G >= 8) v += k >= 4 ? __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false) : 0;
+    if constexpr (G >= 16) v += k >= 8 ? __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false) : 0;
+    return v;
+}
+
+// f(integral_constant<int, J>) for J = 0 .. N-1, unrolled at compile time
+template <typename F, int... I>
+__device__ __forceinline__ void unroll_seq(F &&f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void unroll(F &&f)
+{
+    unroll_seq(f, std::make_integer_sequence<int, N>{});
+}
+
 // number of zero bytes of x (exact: no borrow between bytes)
 __device__ __forceinline__ int zero_bytes(uint32_t x)
 {
@@ -207,19 +222,12 @@ __device__ __forceinline__ int zero_bytes(uint32_t x)
 }
 
 // Observation stores (the step's bulk output, 2/3 of its bytes) as
-// non-temporal stores (SNAKE_OBS_NT): streamed past the caches, so they do not
-// evict the env state the next step's k_logic reads.
-#ifndef SNAKE_OBS_NT
-#define SNAKE_OBS_NT 1
-#endif
+// non-temporal stores: streamed past the caches, so they do not evict the env
+// state the next step's k_logic reads (cfg3 0.0929 -> 0.0908 ms, round 3).
 template <typename T>
 __device__ __forceinline__ void obs_store(T *p, const T &v)
 {
-#if SNAKE_OBS_NT
     __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
 }
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
@@ -399,27 +407,12 @@ __device__ __forceinline__ void perm_record(int ii, int w, int S, NP *link, lu16
 // indices' offsets, and the draw record is written through a per-lane dummy
 // slot instead of exec masking: under the step's load the worker waves are
 // issue-bound, so instructions (SALU and branches included) are the cost.
-#ifndef SNAKE_DR_VPOPC
-#define SNAKE_DR_VPOPC 1
-#endif
-#ifndef SNAKE_DR_CLZ
-#define SNAKE_DR_CLZ 1
-#endif
-#ifndef SNAKE_DR_PAIRLOOP
-#define SNAKE_DR_PAIRLOOP 1
-#endif
-
 // population count of a wave mask on the vector ALU (`ones` is an opaque
 // all-ones VGPR): the scalar count of a mask a vector compare just wrote costs a
 // vector-to-scalar hand-off and a move back in the round's dependency chain
 __device__ __forceinline__ int vpopc(unsigned long long x, uint32_t ones)
 {
-#if SNAKE_DR_VPOPC
     return __builtin_popcount((uint32_t)x & ones) + __builtin_popcount((uint32_t)(x >> 32) & ones);
-#else
-    (void)ones;
-    return __popcll(x);
-#endif
 }
 
 // Returns true when the round ended at a bracket cut inside the pair with
@@ -495,32 +488,18 @@ __device__ __forceinline__ bool draw_round(uint32_t tw0, uint32_t tw1, int base,
     }
     m.pos = base + end;
     i -= A;
-#if SNAKE_DR_CLZ
     // the bracket of the new i, branch-free (i < 1 ends the draws anyway)
     mask = i > 0 ? (0xffffffffu >> __builtin_clz((uint32_t)i)) : 0u;
     lo = (int)(mask >> 1) + 1;
-#else
-    if (__builtin_expect(i < lo, 0)) {   // next power-of-two bracket (i < 1 ends the draws anyway)
-        mask = gen_mask((uint32_t)i);
-        lo = (int)(mask >> 1) + 1;
-    }
-#endif
     return cut && i >= 1 && end < 128 && m.pos < kMtN;
 }
 
 
-// i_start >= 0 resumes a paused attempt at draw index i_start (the MT state in
-// m is the one it was paused with). With a deadline (s_memrealtime ticks, 0 =
-// none) the draws pause between key blocks once it has passed -- never before
-// the first block, so every call makes progress -- and the next draw index is
-// returned (0: the draws are done).
 template <typename NP>
-__device__ int mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, int lane,
-                             int e = -1, int i_start = -1, unsigned long long deadline = 0)
+__device__ void mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, int lane)
 {
-    int i = i_start >= 0 ? i_start : n - 1;
-    if (i < 1) return 0;
-    COUNT_DECL;
+    int i = n - 1;
+    if (i < 1) return;
     uint32_t mask = gen_mask((uint32_t)i);
     int lo = (int)(mask >> 1) + 1;
     // the tempered key stays in registers: the rounds never read LDS, so nothing
@@ -536,38 +515,23 @@ __device__ int mt_perm_draws(WaveMT &m, int n, int S, NP *link, int link_n, lu16
     // invariant ends the wave instead of hanging the GPU
     for (int guard = 0; i >= 1 && guard < (1 << 20); guard++) {
         if (m.pos >= kMtN) {
-            if (deadline && guard > 0 && __builtin_amdgcn_s_memrealtime() > deadline) {
-                COUNT_FLUSH(e, lane);
-                return i;   // paused: m holds the untwisted key, m.pos >= 624
-            }
             mt_twist(m, lane);
 #pragma unroll
             for (int t = 0; t < 10; t++) tk[t] = temper(m.w[t]);
-            COUNT(e, lane, 0);
         }
 #pragma unroll
         for (int q = 0; q < 5; q++) {
-#if SNAKE_DR_PAIRLOOP
             // a round normally consumes the rest of the pair; only a bracket cut
             // inside it repeats the pair
             if (i >= 1 && m.pos < kMtN && (m.pos >> 7) == q) {
                 bool again;
                 do {
-                    COUNT(e, lane, 1);
                     again = draw_round(tk[2 * q], tk[2 * q + 1], q << 7, m, i, mask, lo, S, link, dummy, jsmall,
                                        ones, lane);
                 } while (__builtin_expect(again, 0));
             }
-#else
-            while (i >= 1 && m.pos < kMtN && (m.pos >> 7) == q) {
-                COUNT(e, lane, 1);
-                draw_round(tk[2 * q], tk[2 * q + 1], q << 7, m, i, mask, lo, S, link, dummy, jsmall, ones, lane);
-            }
-#endif
         }
     }
-    COUNT_FLUSH(e, lane);
-    return 0;
 }
 
 // Final arr[k] of the Fisher-Yates pass for k < S from the LDS draw record
@@ -729,12 +693,6 @@ __device__ void place_fruits_fresh(const KCfg &c, uint8_t *g, WaveMT &m, int k, 
     wave_sync();
 }
 
-#ifndef SNAKE_RESET_ROWS
-#define SNAKE_RESET_ROWS 0
-#endif
-#ifndef SNAKE_FRESH_FRUITS
-#define SNAKE_FRESH_FRUITS 1
-#endif
 // ------------------------------------------------------------------ encode
 // _encode (snake_env.py:474-519) + frame stack (:444-472): for snake k the 8
 // channels [wall, fruit, other head/body/tail, own head/body/tail]; with a vision
@@ -939,75 +897,10 @@ __device__ void encode_rows(const KCfg &c, const uint8_t *frames, const int *org
     }
 }
 
-// Row-wise encode of a one-frame stack (fs == 1), with few LDS instructions:
-// lane = one (snake, window row), whose ow output cells are 8*ow contiguous
-// bytes of the staged image. The row's grid bytes come in as dwords (two
-// per 4 cells, realigned with v_alignbyte), each cell's 8 channels are built in
-// a register pair, branch-free, and stored whole (one ds_write_b64 per cell),
-// so the stage needs no zeroing pass and no per-cell byte stores; cells outside
-// the grid write zeros. encode_rows does the same with one LDS byte read and
-// (non-empty cells) one byte store per cell plus a zeroing pass: about 2.5x the
-// LDS instructions, which the concurrent reset workers compete for.
-#ifndef SNAKE_ROWS1
-#define SNAKE_ROWS1 1
-#endif
-__device__ void encode_rows1(const KCfg &c, const uint8_t *frames, const int *org, uint8_t *obs_env,
-                             uint8_t *stage, int lane)
-{
-    const int ow = c.ow, oh = c.oh, S = c.S, W = c.W, H = c.H;
-    const int rowb = ow * 8, P = oh * rowb;
-    const int nd = c.grid_stride >> 2;   // frame dwords (reads are clamped into the frame)
-    const uint32_t *f32 = reinterpret_cast<const uint32_t *>(frames);
-    const bool wide = (c.units & 1) == 0;
-    for (int k0 = 0; k0 < S; k0 += c.enc_group) {
-        const int gs = min(c.enc_group, S - k0), bytes = gs * P;
-        for (int rr = lane; rr < gs * oh; rr += kWave) {
-            const int kk = (int)__umulhi((uint32_t)rr, c.mag_oh), i = rr - kk * oh;
-            const int k = k0 + kk;
-            const int p = org[k];
-            const int r = (p >> 16) - 256 + i, c0 = (p & 0xffff) - 256;
-            const bool rok = (unsigned)r < (unsigned)H;
-            const int a = r * W + c0;          // grid byte of window cell 0
-            const int d0 = a >> 2;              // (floor: a may be negative)
-            const uint32_t sh = (uint32_t)(a & 3);   // (alignbyte shifts by bytes)
-            uint8_t *dst = stage + kk * P + i * rowb;
-            uint32_t lo_w = f32[min(max(d0, 0), nd - 1)];
-            for (int jb = 0; jb < ow; jb += 4) {
-                const uint32_t hi_w = f32[min(max(d0 + (jb >> 2) + 1, 0), nd - 1)];
-                const uint32_t w = __builtin_amdgcn_alignbyte(hi_w, lo_w, sh);   // grid bytes a+jb .. a+jb+3
-                lo_w = hi_w;
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int j = jb + u, col = c0 + j;
-                    const int v = (rok && (unsigned)col < (unsigned)W) ? (int)((w >> (8 * u)) & 255u) : 0;
-                    const int id = div10(v), code = v - 10 * id;
-                    const int ch = (v < 3) ? v - 1 : code - 1 + ((id == k) ? 3 : 0);
-                    const uint32_t bit = (uint32_t)min(v, 1) << (8 * (ch & 3));
-                    uint2 cell;
-                    cell.x = ch < 4 ? bit : 0u;
-                    cell.y = ch < 4 ? 0u : bit;
-                    if (j < ow) *reinterpret_cast<uint2 *>(dst + j * 8) = cell;
-                }
-            }
-        }
-        wave_sync();
-        uint8_t *out = obs_env + (int64_t)k0 * P;
-        if (wide) {
-            for (int q = lane; q < bytes >> 4; q += kWave)
-                obs_store(reinterpret_cast<v4u *>(out) + q, reinterpret_cast<const v4u *>(stage)[q]);
-        } else {
-            for (int q = lane; q < bytes >> 3; q += kWave)
-                obs_store(reinterpret_cast<v2u *>(out) + q, reinterpret_cast<const v2u *>(stage)[q]);
-        }
-        wave_sync();
-    }
-}
-
 __device__ __forceinline__ void encode_obs(const KCfg &c, const uint8_t *frames, const int *org, int slot0,
                                            uint8_t *obs_env, uint8_t *lds, int lane)
 {
-    if (SNAKE_ROWS1 && c.enc_group > 0 && c.fs == 1 && c.rows1) encode_rows1(c, frames, org, obs_env, lds + c.lds_stage, lane);
-    else if (c.enc_group > 0) encode_rows(c, frames, org, slot0, obs_env, lds + c.lds_stage, lane);
+    if (c.enc_group > 0) encode_rows(c, frames, org, slot0, obs_env, lds + c.lds_stage, lane);
     else encode(c, frames, org, slot0, obs_env, lane);
 }
 
@@ -1022,58 +915,20 @@ __device__ __forceinline__ int dir_of_diff(int diff, int W)
 }
 
 // ------------------------------------------------------------------- reset
-// SnakeEnv.reset (snake_env.py:131-159): walled grid, S spawn poses =
-// permutation(n_cand)[:S] retried until disjoint (:576-589), Snake(idx, coords)
-// (core/snake.py:53-74), num_fruits fruit draws, first observation replicated
-// over the frame stack.
 // One iteration of _generate_snakes' retry loop (:576-589): S spawn poses =
 // permutation(n_cand)[:S] drawn from the wave's MT, lane (sk, si) = cell si of
 // pose sk (-1 past S*L), q = the pose indices; true when the poses are disjoint
 // (_clear_overlap :568-574).
-// Draws [lo, hi] of env e's paused attempt, LDS record -> st.spawn_draws.
-__device__ void save_draws(const KCfg &c, const snake_state &st, int e, const lu16 *jarr, int lo, int hi,
-                           int lane)
-{
-    uint16_t *g = st.spawn_draws + (int64_t)e * c.draws_stride;
-    for (int x = lo + lane; x <= hi; x += kWave) g[x] = jarr[x];
-}
-
-// Draws [lo, n) of env e's earlier slices, st.spawn_draws -> the LDS record:
-// 8-byte chunks from the first aligned index (past n only the record's dummy
-// slots are overwritten), single entries below it.
-__device__ void load_draws(const KCfg &c, const snake_state &st, int e, lu16 *jarr, int lo, int lane)
-{
-    const uint16_t *g = st.spawn_draws + (int64_t)e * c.draws_stride;
-    const int lo4 = min((lo + 3) & ~3, c.n_cand);
-    if (lane < lo4 - lo) jarr[lo + lane] = g[lo + lane];
-    const uint64_t *g8 = reinterpret_cast<const uint64_t *>(g);
-    typedef __attribute__((address_space(3))) uint64_t lu64;
-    lu64 *j8 = (lu64 *)jarr;
-    for (int x = (lo4 >> 2) + lane; x < (c.n_cand + 3) >> 2; x += kWave) j8[x] = g8[x];
-}
-
-// One permutation attempt; i_start >= 0 resumes a paused one (its earlier
-// draws in st.spawn_draws). With a deadline the draws may pause: paused_i = the
-// next draw index (> 0), the attempt's own draws are in the LDS record at
-// indices (paused_i, top] and q/cell are not set; the caller saves the state.
 template <int MS, bool JL>
 __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, uint8_t *lds, int slot,
-                              int e, int attempt, int (&q)[MS], int &cell, int lane, int i_start = -1,
-                              unsigned long long deadline = 0, int *paused_i = nullptr)
+                              int (&q)[MS], int &cell, int lane)
 {
     const int S = c.S, L = c.L, SL = S * L;
     const int sk = lane / L, si = lane - sk * L;
-    STAMP(e, lane, 1 + 3 * min(attempt, 3));
     if constexpr (JL) {
         // the u16 draw record in LDS: every index 1..n-1 is written, nothing to clear
         lu16 *jarr = (lu16 *)(lds + c.lds_link);
-        const int pi = mt_perm_draws(mt, c.n_cand, S, jarr, c.n_cand, jarr, lane, e, i_start, deadline);
-        if (pi > 0) {
-            *paused_i = pi;
-            return false;
-        }
-        if (i_start >= 0 && i_start < c.n_cand - 1) load_draws(c, st, e, jarr, i_start + 1, lane);
-        STAMP(e, lane, 2 + 3 * min(attempt, 3));
+        mt_perm_draws(mt, c.n_cand, S, jarr, c.n_cand, jarr, lane);
         wave_sync();
         perm_trace_j<MS>(S, c.n_cand, jarr, q, lane);
     } else {
@@ -1086,12 +941,10 @@ __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, 
         // and made visible, no workgroup barrier -- k_post_lean runs four
         // independent workers per workgroup)
         link_sync();
-        mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, lane, e);
-        STAMP(e, lane, 2 + 3 * min(attempt, 3));
+        mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, lane);
         link_sync();   // the link table, written by every lane
         perm_trace<MS>(S, link, jsmall, q, lane);
     }
-    STAMP(e, lane, 3 + 3 * min(attempt, 3));
     int pk = 0;
 #pragma unroll
     for (int k = 0; k < MS; k++) pk = (sk == k) ? q[k] : pk;
@@ -1175,12 +1028,11 @@ __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &
 // over the frame stack. `mt` comes from load_reset_mt: with a ready spawn-ahead
 // record the poses are the record's and the draws are already done; a partial
 // record continues the retries where the record left them.
-template <int MS, bool JL, bool SLICE>
+template <int MS, bool JL>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
-                         WaveMT &mt, uint8_t *lds, int slot, int spw, int lane, int ps = -1)
+                         WaveMT &mt, uint8_t *lds, int slot, int spw, int lane)
 {
     const int spst = spw & 3;
-    RPROF_VAL(ps, 4, spst, lane);
     uint8_t *frames = lds + c.lds_frames;
     int *org = reinterpret_cast<int *>(lds + c.lds_centers);
     uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
@@ -1202,14 +1054,10 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         // likelier than ~1e-6 per reset)
         int q[MS];
         bool ok = false;
-        // a paused spawn-ahead attempt is finished first (from its draw index)
-        // (only sliced configurations pause attempts: SLICE)
-        const int i0 = SLICE && spst == SPAWN_INPROG ? (int)st.spawn[(int64_t)e * kSpawnStride + kSpawnI] : -1;
         for (int attempt = 0; attempt < (1 << 16) && !ok; attempt++)
-            ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, attempt, q, cell, lane, attempt == 0 ? i0 : -1);
+            ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, q, cell, lane);
         failed = !ok;
     }
-    RPROF(ps, 0, lane);
     // make_grid (grid_util.py:14-20), then paint (:138-144)
     for (int x = lane; x < c.HW; x += kWave) {
         const int r = (int)__umulhi((uint32_t)x, c.mag_W), cc = x - r * W;   // x / W
@@ -1247,15 +1095,8 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         }
     }
     wave_sync();
-    STAMP(e, lane, 20);
-    RPROF(ps, 1, lane);
-#if SNAKE_FRESH_FRUITS
     if (!failed) place_fruits_fresh(c, work, mt, c.num_fruits, cell, lane);   // :147-148
-    else
-#endif
-    place_fruits(c, work, mt, c.num_fruits, fbuf, lane);         // (overlapping snakes: count the grid)
-    STAMP(e, lane, 21);
-    RPROF(ps, 2, lane);
+    else place_fruits(c, work, mt, c.num_fruits, fbuf, lane);     // (overlapping snakes: count the grid)
     uint8_t *gbase = st.grid + (int64_t)e * c.fs * c.grid_stride;
     const int n16 = c.grid_stride >> 4;
     for (int q = lane; q < n16; q += kWave) {
@@ -1271,25 +1112,14 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
         if (c.bg) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)((((uint32_t)spw >> 3) + 1u) << 3);
         else if (spst != SPAWN_NONE) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spw & ~3;
         st.env[(int64_t)e * kEnvRec + ENV_FAIL] = failed ? 1 : 0;
-        st.env[(int64_t)e * kEnvRec + ENV_VOID] = 0;
         if (failed && o.err) o.err[e] = 2;
     }
     if (lane < 2 * S) reinterpret_cast<uint64_t *>(st.stats)[(int64_t)e * 2 * S + lane] = 0ull;   // _reset_epi_stats
     mt_store(mt, st.mt + (int64_t)e * kMtN, lane);
     wave_sync();
-    STAMP(e, lane, 22);
-    RPROF(ps, 3, lane);
-    // One env's obs is on the reset's critical path: up to 4 KB (cfg3's 3 872 B)
-    // the direct encode, where the staged row-wise encode's two extra LDS passes
-    // cost more than they save; larger observations (full maps, frame stacks)
-    // through the staging buffer, which the draw record no longer needs.
-#if SNAKE_RESET_ROWS
-    if (c.enc_group > 0 && c.units * 8 > 4096) encode_rows(c, frames, org, 0, o.obs + (int64_t)e * c.units * 8,
-                                                           lds + c.lds_stage, lane);
-    else
-#endif
+    // (the direct encode: on the reset's critical path the staged row-wise
+    // encode's two extra LDS passes cost more than they save)
     encode(c, frames, org, 0, o.obs + (int64_t)e * c.units * 8, lane);
-    STAMP(e, lane, 23);
 }
 
 // -------------------------------------------------------------------- step
@@ -1322,8 +1152,10 @@ __device__ __forceinline__ void stage_to_lds(uint8_t *dst, const uint8_t *src, i
 // auto-reset. The wave-wide parts (dying-body erase, fruit respawn) loop over the
 // block's envs that need them.
 template <int MS>
-__global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
+__global__ void __launch_bounds__(64) k_logic(const KArgs)
 {
+    WTIME(0);
+    LSTAMP(40);
     const KArgs &A = kargs();
     const KCfg &c = A.c;
     const snake_state &st = A.st;
@@ -1348,8 +1180,6 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     // step, the next step's k_autoreset)
     int *qb = st.resetq + (int64_t)c.qpar * (kNumQ * kQShards * c.q_cap + kQCounters);
     int *qcnt = qb + kNumQ * kQShards * c.q_cap;
-    LSTAMP(40);
-    OBSMIN(1400, lane);
     auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
     // ---- every load this step needs, issued up front
@@ -1360,10 +1190,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
         // still void a record its fruit draws make stale
         er2 = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec + 4);
     }
-#ifndef SNAKE_VOID
-#define SNAKE_VOID 1
-#endif
-    const int spst = er2.x & 3, voided = SNAKE_VOID ? er2.z : 0;   // ENV_SPAWN, ENV_VOID
+    const int spst = er2.x & 3;   // ENV_SPAWN
     int4 rec = make_int4(0, 0, 0, 0);
     int act = 0;
     // the snake's running episode statistics, one 16-byte record (snake_epi_stat)
@@ -1407,9 +1234,11 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     };
     if (fs == 1) stage(std::true_type{});
     else stage(std::false_type{});
+    LSTAMP(51);
     // keep the statistics loads up here with the others (the compiler would sink
     // them to their first use, deep in the step, and pay a full memory latency there)
     __asm__ volatile("" ::"v"(sv.x), "v"(sv.y), "v"(sv.z), "v"(sv.w));
+    LSTAMP(52);
     double s0 = __hiloint2double((int)sv.y, (int)sv.x);
     uint32_t s1 = sv.z, s2 = sv.w & 0xffffu, s3 = sv.w >> 16;
     const int ncur = (fs == 1) ? 0 : (cur + 1 == fs ? 0 : cur + 1);
@@ -1451,13 +1280,14 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     LSTAMP(41);
 
     // _check_collision :521-544 -- groups of snakes with the same target cell
+    // (lanes k >= S hold no snake: their ncell -1 - lane matches nothing)
     int cnt = 0;
     bool lower = false;
-    for (int j = 0; j < S; j++) {
-        const bool same = __shfl(ncell, gb + j) == ncell;
+    unroll<G>([&](auto J) {
+        const bool same = gsel<G, J>(ncell) == ncell;
         cnt += same;
-        lower |= same && j < k;
-    }
+        lower |= same && J < k;
+    });
     const bool leader = mv && !lower;
     const int v = mv ? work[ncell] : 0;
     const int vid = div10(v), cv = v - 10 * vid;
@@ -1469,17 +1299,17 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     // kill credit: one per deadly group on a BODY/HEAD cell, to its owner (self too)
     const int owner = (leader && deadly && (cv == C_BODY || cv == C_HEAD)) ? vid : -1;
     int kills = 0;
-    for (int j = 0; j < S; j++) kills += __shfl(owner, gb + j) == k;
+    unroll<G>([&](auto J) { kills += gsel<G, J>(owner) == k; });   // (owner -1 off the snakes)
     int alive_snakes = alive0 - __popc(gbits(__ballot(deadly)));            // :334
     bool death = deadly;
     // :338-346 a fruit eater's tail does not move: snakes entering it die (again)
     const int etail = eat ? tr * W + tc : -2;
     bool hit = false;
-    for (int j = 0; j < S; j++) {
-        const int ej = __shfl(etail, gb + j), nj = __shfl(ncell, gb + j);
+    unroll<G>([&](auto J) {   // (off the snakes: etail -2, ncell -1 - lane)
+        const int ej = gsel<G, J>(etail), nj = gsel<G, J>(ncell);
         hit |= mv && ej == ncell;
         kills += (eat && nj == etail) ? 1 : 0;
-    }
+    });
     alive_snakes -= __popc(gbits(__ballot(hit)));
     death |= hit;
     alive = mv && !death;
@@ -1532,7 +1362,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     // urgent (at most one live snake: the reset is likely next) and other jobs
     const bool urgent = __popc(am) <= 1;
     const bool spawn_q = c.spawn_thr >= 0 && env_ok && !bad && !ep_end && (need ? true : spst != SPAWN_READY) &&
-                         __popc(am) <= c.spawn_thr && (!c.spawn_redo || urgent || !voided);
+                         __popc(am) <= c.spawn_thr;
     const unsigned long long pm = __ballot(spawn_q && urgent && k == 0);
     const unsigned long long pn = __ballot(spawn_q && !urgent && k == 0);
     int pbase = 0, nbase = 0;
@@ -1547,9 +1377,12 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     uint64_t rchunk = 0;
     if (refill) rchunk = *reinterpret_cast<const uint64_t *>(ring + rbase);
     const bool dying = isn && death;
-    int dd[16];
-#pragma unroll
-    for (int t = 0; t < 16; t++) dd[t] = (dying && t < rl - 1) ? ring[(rh + t) & (cap - 1)] : 0;
+    // (the two aligned 16-byte ring chunks that hold positions rh .. rh + 15)
+    uint4 dc0 = make_uint4(0, 0, 0, 0), dc1 = make_uint4(0, 0, 0, 0);
+    if (dying) {
+        dc0 = *reinterpret_cast<const uint4 *>(ring + (rh & (cap - 16)));
+        dc1 = *reinterpret_cast<const uint4 *>(ring + ((rh + 16) & (cap - 16)));
+    }
     // the next G * kRespawnT raw words of the stream; past the key's end they
     // are words of the next key, computed from the old one (new[j] for j < 227
     // needs old[j], old[j+1] and old[j+397] only): the twist is left pending in
@@ -1649,7 +1482,16 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
         for (int m0 = 0; m0 < n; m0 += 16) {
             int d[16];
 #pragma unroll
-            for (int t = 0; t < 16; t++) d[t] = (m0 == 0) ? dd[t] : ((m0 + t < n) ? rk[(rh + m0 + t) & (cap - 1)] : 0);
+            for (int t = 0; t < 16; t++) {
+                if (m0 == 0) {   // from the two chunks loaded with the second round
+                    const int x = (rh & 15) + t;
+                    const uint32_t w = x < 16 ? (x < 8 ? (x < 4 ? dc0.x : dc0.y) : (x < 12 ? dc0.z : dc0.w))
+                                              : (x < 24 ? (x < 20 ? dc1.x : dc1.y) : (x < 28 ? dc1.z : dc1.w));
+                    d[t] = t < n ? (int)((w >> (8 * (x & 3))) & 255u) : 0;
+                } else {
+                    d[t] = (m0 + t < n) ? rk[(rh + m0 + t) & (cap - 1)] : 0;
+                }
+            }
             if (m0 == 0 && (rh & 3) != 0) {                          // the pending head-word bytes
 #pragma unroll
                 for (int t = 0; t < 3; t++)
@@ -1678,21 +1520,31 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     // (per env, all G lanes of the group, snake or not: the empties are counted by all)
     bool fast_done = false;
     if (__ballot(need)) {
-        const int HW = c.HW, nw = (HW + 3) >> 2, wpl = (nw + G - 1) / G;
-        const int w0 = min(nw, k * wpl), w1 = min(nw, w0 + wpl);
-        const uint32_t *gw = reinterpret_cast<const uint32_t *>(work);
+        // lane k of the group counts the empty cells of its slice of 16-byte
+        // chunks (bytes past the grid count as occupied)
+        const int HW = c.HW, nc = (HW + 15) >> 4, cpl = (nc + G - 1) / G;
+        const int q0 = min(nc, k * cpl), q1 = min(nc, q0 + cpl);
+        auto chunk = [&](int q) {
+            uint4 x = reinterpret_cast<const uint4 *>(work)[q];
+            if (q == nc - 1 && (HW & 15)) {
+                const int r = HW & 15;
+                x.x |= r >= 4 ? 0u : 0xffffffffu << (8 * r);
+                x.y |= r >= 8 ? 0u : (r <= 4 ? 0xffffffffu : 0xffffffffu << (8 * (r - 4)));
+                x.z |= r >= 12 ? 0u : (r <= 8 ? 0xffffffffu : 0xffffffffu << (8 * (r - 8)));
+                x.w |= r <= 12 ? 0xffffffffu : 0xffffffffu << (8 * (r - 12));
+            }
+            return x;
+        };
         int cnt = 0;
         if (need) {
-            for (int w = w0; w < w1; w++) {
-                uint32_t x = gw[w];
-                if (w == nw - 1 && (HW & 3)) x |= 0xffffffffu << (8 * (HW & 3));   // past the grid
-                cnt += zero_bytes(x);
+            for (int q = q0; q < q1; q++) {
+                const uint4 x = chunk(q);
+                cnt += zero_bytes(x.x) + zero_bytes(x.y) + zero_bytes(x.z) + zero_bytes(x.w);
             }
         }
-        const int incl = wave_scan(cnt, lane);
-        const int gbase = __shfl(incl - cnt, gb);
-        const int excl = incl - cnt - gbase;
-        const int Etot = __shfl(incl, gb + G - 1) - gbase;
+        const int incl = gscan<G>(cnt, k);
+        const int excl = incl - cnt;
+        const int Etot = gsel<G, G - 1>(incl);
         const uint32_t rng = (uint32_t)(Etot - 1), rmask = gen_mask(rng);
         // rng == 0 draws nothing (randint(0, 1) consumes no raw word)
         const bool draws = need && Etot > 0 && rng != 0;
@@ -1720,19 +1572,24 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
             }
             if (act_d && v >= excl && v < excl + cnt) {      // this lane's slice holds it
                 int need_n = v - excl, x = -1;
-                for (int w = w0; w < w1 && x < 0; w++) {
-                    uint32_t y = gw[w];
-                    if (w == nw - 1 && (HW & 3)) y |= 0xffffffffu << (8 * (HW & 3));
-                    const int z = zero_bytes(y);
-                    if (need_n < z) {
-                        for (int b = 0; b < 4; b++) {
-                            if (((y >> (8 * b)) & 255u) == 0u) {
-                                if (need_n == 0) { x = 4 * w + b; break; }
-                                need_n--;
-                            }
+                for (int q = q0; q < q1 && x < 0; q++) {
+                    const uint4 y4 = chunk(q);
+                    const int z0 = zero_bytes(y4.x), z1 = zero_bytes(y4.y), z2 = zero_bytes(y4.z), z3 = zero_bytes(y4.w);
+                    if (need_n >= z0 + z1 + z2 + z3) {
+                        need_n -= z0 + z1 + z2 + z3;
+                        continue;
+                    }
+                    // the dword, then the byte
+                    int dw = 0;
+                    uint32_t y = y4.x;
+                    if (need_n >= z0) { need_n -= z0; dw = 1; y = y4.y;
+                        if (need_n >= z1) { need_n -= z1; dw = 2; y = y4.z;
+                            if (need_n >= z2) { need_n -= z2; dw = 3; y = y4.w; } } }
+                    for (int b = 0; b < 4; b++) {
+                        if (((y >> (8 * b)) & 255u) == 0u) {
+                            if (need_n == 0) { x = 16 * q + 4 * dw + b; break; }
+                            need_n--;
                         }
-                    } else {
-                        need_n -= z;
                     }
                 }
                 cellbuf[d] = (uint16_t)x;
@@ -1765,7 +1622,6 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
     // first, is overwritten here; so with bg every draw writes the word)
     const bool spw_wr = drew && (c.bg || spst != SPAWN_NONE);
     const uint32_t spw1 = drew ? (((uint32_t)er2.x >> 3) + 1u) << 3 : (uint32_t)er2.x;
-    const int voided1 = (drew && spst != SPAWN_NONE) ? 1 : voided;   // (a record was wasted this episode)
 
     LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
@@ -1803,10 +1659,9 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
         if (c.bg) atomicExch(reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN), spw1);
         else st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)spw1;
     }
-    if (SNAKE_VOID && env_ok && k == 0 && !bad && voided1 != voided) st.env[(int64_t)e * kEnvRec + ENV_VOID] = voided1;
     LSTAMP(49);
     int rank = 1;
-    for (int j = 0; j < S; j++) rank += (__shfl(s0, gb + j) > s0);
+    unroll<G>([&](auto J) { rank += (J < S && gsel<G, J>(s0) > s0) ? 1 : 0; });
     if (isn && ep_end) {   // the episode summary where it ended (nothing stored elsewhere:
                            // ~1.5 % of the envs at cfg3, 9.4 of k_logic's MB per step)
         o.rank[(int64_t)e * S + k] = rank;
@@ -1853,7 +1708,7 @@ __global__ void __launch_bounds__(64, SNAKE_STEP_MIN_WAVES) k_logic(const KArgs)
         reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + k] = nrec;
     }
     LSTAMP(47);
-    OBSMAX(1401, lane);
+    WTIME(1);
 }
 
 // ---------------------------------------------------- step: the observation
@@ -1897,33 +1752,16 @@ __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, 
     }
 }
 
-// With a deadline (the step's spawn-ahead time slice, JL boards only) an
-// attempt still drawing when it passes is paused: its draws so far go to
-// st.spawn_draws, the key and position to the record, the next draw index to
-// record word kSpawnI, status INPROG; a later job (or the env's reset)
-// continues it from there.
-template <int MS, bool JL, bool SLICE>
-__device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot,
-                         unsigned long long deadline, int lane)
+// The in-step spawn-ahead job of env e: one attempt from its MT state or its
+// partial record, into record buffer 0.
+template <int MS, bool JL>
+__device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot, int lane)
 {
     WaveMT mt;
-    const int spw = load_reset_mt(c, st, e, mt, lane), spst = spw & 3;
-    if (spst == SPAWN_READY) return;
-    uint32_t *rec = spawn_rec(c, st, e, 0);
-    const int i0 = spst == SPAWN_INPROG ? (int)rec[kSpawnI] : -1;
-    int q[MS], cell, pi = 0;
-    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, 0, q, cell, lane, i0, SLICE ? deadline : 0ull,
-                                          &pi);
-    if (SLICE && pi > 0) {
-        save_draws(c, st, e, (const lu16 *)(lds + c.lds_link), pi + 1, i0 >= 0 ? i0 : c.n_cand - 1, lane);
-        mt_store(mt, rec, lane);
-        if (lane == 0) {
-            rec[kSpawnPos] = (uint32_t)mt.pos;
-            rec[kSpawnI] = (uint32_t)pi;
-            st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (spw & ~7) | SPAWN_INPROG;
-        }
-        return;
-    }
+    const int spw = load_reset_mt(c, st, e, mt, lane);
+    if ((spw & 3) == SPAWN_READY) return;
+    int q[MS], cell;
+    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, q, cell, lane);
     store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)spw);
 }
 
@@ -1956,7 +1794,7 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
     bool ok = false;
     for (int a = 0; a < c.bg_tries && !ok; a++) {   // (attempts until disjoint, at most bg_tries)
         if (a > 0) wave_sync();
-        ok = spawn_attempt<MS, true>(c, st, mt, lds, 0, e, a, q, cell, lane);
+        ok = spawn_attempt<MS, true>(c, st, mt, lds, 0, q, cell, lane);
     }
     store_spawn_record<MS, true>(c, st, e, mt, ok, q, lane, spw, buf ^ 1);
 }
@@ -1976,7 +1814,7 @@ __device__ void spawn_after_reset(const KCfg &c, const snake_state &st, int e, W
     int q[MS], cell;
     bool ok = false;
     for (int a = 0; a < kResetAheadTries && !ok; a++)
-        ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, e, a, q, cell, lane);
+        ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, q, cell, lane);
     store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)st.env[(int64_t)e * kEnvRec + ENV_SPAWN], 0);
 }
 
@@ -2009,18 +1847,13 @@ __device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st,
 // fewer registers. JL: the draw record in LDS (KCfg.link_in_lds), else the
 // global link tables; one path per instantiation.
 // wid = this worker (0 .. G-1): k_autoreset's block, or a block of k_post.
-template <int MS, bool SLICE, bool RO, bool JL>
+template <int MS, bool RO, bool JL>
 __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uint8_t *lds)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const KArgs &A = kargs();
     const KCfg &c = A.c;
     const snake_state &st = A.st;
-    // the spawn-ahead time slice of this step (KCfg.spawn_budget, SLICE only): no
-    // spawn job starts after it, and attempts still drawing pause at it
-    const unsigned long long deadline =
-        SLICE ? __builtin_amdgcn_s_memrealtime() + (unsigned long long)c.spawn_budget : 0ull;
-    OBSMIN(1406, lane);
     // the shard counts of the three queues, prefix-summed: queue index j lives
     // in the shard whose [excl, incl) holds it
     const int64_t qset = kNumQ * kQShards * c.q_cap + kQCounters;
@@ -2033,13 +1866,12 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
     // claim shards: min(G, kClaimShards), so that every shard has a worker
     const int nsh = min(G, kClaimShards);
     const int x = G >= kClaimShards ? (wid & (kClaimShards - 1)) : wid % nsh;
-    // spawn_cap: the other (2-live-snake) jobs only as far as the first round
-    // of workers reaches; their envs are queued again next step
-    int Nn = bcast(nincl, kWave - 1);
-    if (c.spawn_cap) Nn = min(Nn, max(G - R - U, 0));
-    const int P = (RO || c.bg) ? 0 : U + Nn;   // (background: the spawn jobs are k_spawn's)
+    const int P = (RO || c.bg) ? 0 : U + bcast(nincl, kWave - 1);   // (background: the spawn jobs are k_spawn's)
     const int T = R + P;
-    if (wid == 0 && lane == 0 && R > 0) atomicAdd(&g_resets_run, (unsigned long long)R);
+    if (wid == 0 && lane == 0 && R > 0) {
+        atomicAdd(&g_resets_run, (unsigned long long)R);
+        if (c.diag) atomicAdd(&g_resets_timed, (unsigned long long)R);
+    }
     // env of job j of queue q
     // (only the inclusive prefix sums stay live across the jobs: the shard of
     // job j is the number of shards whose prefix ends at or before j)
@@ -2068,22 +1900,15 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
             WaveMT mt;
             const int spst = J.c.bg ? claim_reset_mt(J.c, J.st, e, mt, lane) : load_reset_mt(J.c, J.st, e, mt, lane);
             if (J.c.diag && lane == 0 && (spst & 3) == SPAWN_READY) DIAG_ADD(g_spawn_hits);
-            if (idx < 128) OBSPROF(idx, lane);
-            const int ps = idx < 128 ? idx : -1;
-            do_reset<MS, JL, SLICE && JL>(J.c, J.st, J.o, e, mt, lds, wid, spst, lane, ps);
-            if (idx < 128) OBSPROF(128 + idx, lane);
+            do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, wid, spst, lane);
         } else if (!RO && idx < R + P) {
             if (J.c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
             else if (J.c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(2);
             const int j = idx - R;
             const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
-            if (!SLICE || __builtin_amdgcn_s_memrealtime() < deadline) {   // (else: queued again next step)
-                if (J.c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
-                if (j < 128) OBSPROF(512 + j, lane);
-                do_spawn<MS, JL, SLICE && JL>(J.c, J.st, e, lds, wid, JL ? deadline : 0ull, lane);
-                if (j < 128) OBSPROF(640 + j, lane);
-            }
+            if (J.c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
+            do_spawn<MS, JL>(J.c, J.st, e, lds, wid, lane);
         }
         int v = 0;
         if (lane == 0) v = atomicAdd(&qc[(kQClaim + x) * kQSpread], 1);
@@ -2091,7 +1916,6 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
         idx = G + x + nsh * nx;
         if (idx >= T) break;
     }
-    OBSMAX(1402, lane);
     // Every worker ends with exactly one failing claim, so the shard's claims
     // number its jobs + its workers, and the worker whose failing claim is the
     // shard's last finishes the shard. The last shard to finish re-zeroes the
@@ -2110,11 +1934,11 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
     }
 }
 
-template <int MS, bool SLICE, bool RO, bool JL>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_autoreset(const KArgs)
+template <int MS, bool RO, bool JL>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kResetWavesPerEU))) k_autoreset(const KArgs)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    autoreset_worker<MS, SLICE, RO, JL>((int)blockIdx.x, (int)gridDim.x, lds);
+    autoreset_worker<MS, RO, JL>((int)blockIdx.x, (int)gridDim.x, lds);
 }
 
 // Background spawn-ahead (KCfg.bg): the step's spawn-ahead jobs, run by
@@ -2124,7 +1948,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
 // are claimed on 16 claim shards like k_autoreset's, whose last worker
 // re-zeroes the set's spawn counters.
 template <int MS>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_RESET_WAVES_PER_EU))) k_spawn(const KArgs)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kResetWavesPerEU))) k_spawn(const KArgs)
 {
     const KArgs &A = kargs();
     const KCfg &c = A.c;
@@ -2158,16 +1982,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SNAKE_R
         const int e = ent & ((1 << (32 - kQGenBits)) - 1);
         const uint32_t qgen = (uint32_t)ent >> (32 - kQGenBits);
         if (c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
-        if (idx < 128) OBSPROF(512 + idx, lane);
         const KArgs &J = kargs();
         do_spawn_bg<MS>(J.c, J.st, e, qgen, lds, lane);
-        if (idx < 128) OBSPROF(640 + idx, lane);
         int v = 0;
         if (lane == 0) v = atomicAdd(&qc[(kQSpClaim + x) * kQSpread], 1);
         nx = bcast(v, 0);
         idx = G + x + nsh * nx;
     }
-    OBSMAX(1405, lane);
     // the shard's last claim finishes the shard; the last shard re-zeroes (as in
     // k_autoreset, with this kernel's claim and done counters)
     const int jobs_x = T > G + x ? (T - G - x + nsh - 1) / nsh : 0;
@@ -2186,22 +2007,13 @@ __device__ __forceinline__ void encode_one(const KCfg &c, const snake_state &st,
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x;
-    const bool prof_ = (e & 511) == 0 && (e >> 9) < 128;
-    if (prof_) OBSPROF(256 + (e >> 9), lane);
     // a reset env's obs is written by its reset; in every-step mode only the
     // envs rejected for an invalid action (left unchanged) are not reset
     if (c.autoreset == 2 ? o.err[e] != 1 : (c.autoreset && o.ep_done[e])) return;
     if (c.encode_prio == 1) __builtin_amdgcn_s_setprio(1);      // (setprio takes an immediate)
     else if (c.encode_prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (c.encode_prio == 3) __builtin_amdgcn_s_setprio(3);
-#ifdef SNAKE_ENC_NULL
-    // diagnostic build: the obs bytes stored, nothing read or computed
-    for (int q = lane; q < (c.units * 8) >> 4; q += kWave)
-        reinterpret_cast<uint4 *>(o.obs + (int64_t)e * c.units * 8)[q] = make_uint4(0, 0, 0, 0);
-    return;
-#endif
     encode_env(c, st, o, e, lds, lane);
-    if (prof_) OBSPROF(384 + (e >> 9), lane);
 }
 
 __global__ void __launch_bounds__(64) k_encode(const KCfg c, const snake_state st, const snake_out o)
@@ -2267,25 +2079,20 @@ __device__ __forceinline__ void encode_multi(const KCfg &c, const snake_state &s
 #undef SNAKE_ENC_FETCH
 }
 
-template <int NPF>
-__global__ void __launch_bounds__(64) k_encode_multi(const KCfg c, const snake_state st, const snake_out o)
-{
-    encode_multi<NPF>(c, st, o, (int)blockIdx.x);
-}
-
-// The shared phase as one launch (KCfg.fused): blocks [0, reset_slots) are the
-// reset workers (autoreset_worker), the rest the encodes (NPF = 0: one env per
-// block, encode_one; else encode_multi<NPF>). Dispatched in block order, so the
-// workers go first as on the fork/join path, without the side stream's event
-// round trips on the host and on the device; the kernel's registers and LDS are
-// the larger of the two.
-template <int MS, int NPF, bool RO>
+// The shared phase as one launch: blocks [0, reset_slots) are the reset workers
+// (autoreset_worker), the rest the encodes (NPF = 0: one env per block,
+// encode_one; else encode_multi<NPF>). Dispatched in block order, so the workers
+// go first; one launch instead of a fork onto a side stream and a join (round 3:
+// cfg3 0.0970 -> 0.0941 ms, cfg2 0.0591 -> 0.0539); the kernel's registers and
+// LDS are the larger of the two. JL: the workers' draw record in LDS, else their
+// global link tables (boards of more than 18 368 spawn poses).
+template <int MS, int NPF, bool RO, bool JL>
 __global__ void __launch_bounds__(64) k_post(const KArgs)
 {
     const int G = kargs().c.reset_slots, b = (int)blockIdx.x;
     if (b < G) {
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-        autoreset_worker<MS, false, RO, true>(b, G, lds);
+        autoreset_worker<MS, RO, JL>(b, G, lds);
     } else {
         const KArgs &A = kargs();
         if constexpr (NPF == 0) encode_one(A.c, A.st, A.o, b - G);
@@ -2293,15 +2100,14 @@ __global__ void __launch_bounds__(64) k_post(const KArgs)
     }
 }
 
-// Lean encode over c.enc_per_wave consecutive envs per workgroup of T threads
-// (W % 4 == 0): the next env's frames (NPW dwords per thread), current slot,
-// crop centres and reset flag are loaded into registers while this env is
-// encoded, one memory round trip per env in the shadow of the previous encode;
-// the zero border of the LDS image is written once per workgroup. The LDS
-// destination of every prefetched dword is the same for every env (computed
-// once). T = 64 (one wave per env) for small rings; T = 256 for large ones
-// (cfg5's 40x40 x 4 frames: 1600 dwords): four waves share one LDS image, a
-// quarter of the LDS per wave, and 7 prefetched dwords per thread instead of 25.
+// Lean encode over c.enc_per_wave consecutive envs per workgroup of T = 256
+// threads (W % 4 == 0, rings of 513 to 2 048 dwords: cfg5's 40x40 x 4 frames):
+// the next env's frames (NPW dwords per thread), current slot, crop centres and
+// reset flag are loaded into registers while this env is encoded, one memory
+// round trip per env in the shadow of the previous encode; the zero border of
+// the LDS image is written once per workgroup. The LDS destination of every
+// prefetched dword is the same for every env (computed once). Four waves share
+// one LDS image (cfg5 k_encode 91 -> 66 us against one wave per env, round 3).
 template <int NPW, int T>
 __device__ __forceinline__ void encode_lean_block(const KCfg &c, const snake_state &st, const snake_out &o,
                                                   const int blk)
@@ -2330,7 +2136,6 @@ __device__ __forceinline__ void encode_lean_block(const KCfg &c, const snake_sta
         src[u] = s * gsw + xx;
         dst[u] = (s * c.pframe + (r + c.vr) * c.pw + c.lp) / 4 + c4;
     }
-    OBSMIN(1404, lane);
     zero_lean<T>(c, pf, lane);
     const int e_begin = blk * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
     uint32_t w[NPW];
@@ -2363,30 +2168,25 @@ __device__ __forceinline__ void encode_lean_block(const KCfg &c, const snake_sta
         }
     }
 #undef SNAKE_LEAN_FETCH
-    OBSMAX(1403, lane);
 }
 
-template <int NPW, int T>
-__global__ void __launch_bounds__(T) k_encode_lean(const KCfg c, const snake_state st, const snake_out o)
-{
-    encode_lean_block<NPW, T>(c, st, o, (int)blockIdx.x);
-}
-
-// The shared phase of a background-spawn-ahead board with four-wave lean
-// encodes (cfg5) as one launch (KCfg.post_lean): workgroups [0, ceil(reset_slots
-// / 4)) hold four independent resets-only workers each (wave w of workgroup b
-// is worker 4b + w, with its own KCfg.lds_worker bytes of LDS and, for a reset
-// that finds no ready record, its own global link table: no workgroup barrier
-// on their path), the rest are lean-encode workgroups. No side stream: the
-// fork's and the join's cross-stream latency (12 and 16 us at cfg5) go away.
-template <int MS>
+// The shared phase of a board with four-wave lean encodes (cfg5) as one launch:
+// workgroups [0, ceil(reset_slots / 4)) hold four independent workers each
+// (wave w of workgroup b is worker 4b + w, with its own KCfg.lds_worker bytes of
+// LDS -- frames, centres, fruit buffer, no draw record -- and its own global
+// link table for the attempts it runs: no workgroup barrier on their path), the
+// rest are lean-encode workgroups. RO: background spawn-ahead (the default on
+// these boards), the workers run the resets only; else also the in-step
+// spawn-ahead attempts. One launch instead of the fork/join of round 2 (12 and
+// 16 us of cross-stream latency per step at cfg5).
+template <int MS, bool RO>
 __global__ void __launch_bounds__(256) k_post_lean(const KArgs)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int G = kargs().c.reset_slots, GB = (G + 3) >> 2, b = (int)blockIdx.x;
     if (b < GB) {
         const int wave = (int)(threadIdx.x >> 6), wid = 4 * b + wave;
-        if (wid < G) autoreset_worker<MS, false, true, false>(wid, G, lds + wave * kargs().c.lds_worker);
+        if (wid < G) autoreset_worker<MS, RO, false>(wid, G, lds + wave * kargs().c.lds_worker);
     } else {
         const KArgs &A = kargs();
         encode_lean_block<8, 256>(A.c, A.st, A.o, b - GB);
@@ -2404,10 +2204,9 @@ __global__ void __launch_bounds__(64) k_reset(const KArgs)
         const KArgs &J = kargs();
         const uint8_t *mask = (const uint8_t *)J.aux;
         if (mask && !mask[e]) continue;
-        STAMP(e, lane, 0);
         WaveMT mt;
         const int spst = load_reset_mt(J.c, J.st, e, mt, lane);
-        do_reset<MS, JL, JL>(J.c, J.st, J.o, e, mt, lds, blockIdx.x, spst, lane);
+        do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, blockIdx.x, spst, lane);
         // with spawn-ahead on, the next reset's poses are drawn now, off the step
         const KArgs &J2 = kargs();
         if (J2.c.spawn_thr >= 0) spawn_after_reset<MS, JL>(J2.c, J2.st, e, mt, lds, blockIdx.x, lane);
@@ -2427,7 +2226,6 @@ __global__ void k_seed(const KCfg c, const snake_state st, uint32_t base, long l
     }
     st.env[(int64_t)e * kEnvRec + ENV_MTPOS] = kMtN;
     st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = SPAWN_NONE;
-    st.env[(int64_t)e * kEnvRec + ENV_VOID] = 0;
 }
 
 // rgb_from_grid (grid_util.py:164-175) of every env's current grid: a palette
@@ -2568,24 +2366,33 @@ static int check_launch(const char *what)
     return SNAKE_OK;
 }
 
-// The fork/join events only order kernels of one device: no system-scope fence
-// (that would write the L2s back for a host that never looks). Stream
-// write/wait-value packets on signal memory were tried for the fork/join and
-// measured no faster in the step (scripts/microbench/forkjoin.hip shows them
-// cheaper in isolation).
+// The background stream's events only order kernels of one device: no
+// system-scope fence (that would write the L2s back for a host that never looks).
 constexpr unsigned kJoinFlags = hipEventDisableTiming | hipEventDisableSystemFence;
 
 // Background spawn-ahead (KCfg.bg) per state (keyed by its env records): the
-// stream k_spawn runs on, the event recorded after the last one of each queue
-// set, the step counter whose parity picks the queue set.
+// stream k_spawn runs on, the event the caller's stream records after k_logic
+// (k_spawn's start), the event recorded after the last k_spawn of each queue
+// set, the step counter whose parity picks the queue set. Created by the
+// state's first step, destroyed by snake_release.
 struct BgCtx {
     hipStream_t x = nullptr;
+    hipEvent_t fork = nullptr;
     hipEvent_t done[2] = {nullptr, nullptr};
     uint64_t steps = 0;
     bool pending[2] = {false, false};
 };
 static std::mutex g_bgmu;
 static std::map<const void *, BgCtx> g_bg;
+
+static void destroy_bg(BgCtx &c)
+{
+    if (c.x) (void)hipStreamSynchronize(c.x);   // (its last k_spawn)
+    for (hipEvent_t ev : {c.fork, c.done[0], c.done[1]})
+        if (ev) (void)hipEventDestroy(ev);
+    if (c.x) (void)hipStreamDestroy(c.x);
+    c = BgCtx();
+}
 
 static BgCtx *bg_ctx(const snake_state &st, bool create)
 {
@@ -2594,15 +2401,11 @@ static BgCtx *bg_ctx(const snake_state &st, bool create)
     if (it != g_bg.end()) return &it->second;
     if (!create) return nullptr;
     BgCtx c;
-    static const char *ev_sp = getenv("SNAKE_BG_STREAM_PRIO");   // 1: the lowest, 2: the highest stream priority
-    int least = 0, greatest = 0, prio = 0;
-    if (ev_sp && atoi(ev_sp)) {
-        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-        prio = atoi(ev_sp) == 2 ? greatest : least;
-    }
-    if (hipStreamCreateWithPriority(&c.x, hipStreamNonBlocking, prio) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&c.x, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c.fork, kJoinFlags) != hipSuccess ||
         hipEventCreateWithFlags(&c.done[0], kJoinFlags) != hipSuccess ||
         hipEventCreateWithFlags(&c.done[1], kJoinFlags) != hipSuccess) {
+        destroy_bg(c);
         set_error("background stream / event creation failed");
         return nullptr;
     }
@@ -2620,6 +2423,24 @@ int wait_background(const snake_state &st, void *stream)
             return SNAKE_E_LAUNCH;
         }
     return SNAKE_OK;
+}
+
+// The state's background context (snake_release): its last spawn kernel
+// waited for on the host, its stream and events destroyed, the entry erased,
+// so an allocation that later reuses the same env address starts afresh.
+int release_background(const snake_state &st)
+{
+    BgCtx c;
+    {
+        std::lock_guard<std::mutex> g(g_bgmu);
+        auto it = g_bg.find(st.env);
+        if (it == g_bg.end()) return SNAKE_OK;
+        c = it->second;
+        g_bg.erase(it);
+    }
+    DeviceGuard dg(c.x);   // (the stream's device current while it is destroyed)
+    destroy_bg(c);
+    return dg.dev < 0 ? SNAKE_E_LAUNCH : SNAKE_OK;
 }
 
 int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_t env_offset,
@@ -2672,50 +2493,44 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
     return check_launch("k_reset");
 }
 
-// A side stream and fork/join events per (device, caller stream): k_encode runs
-// on the side stream concurrently with k_autoreset on the caller's stream.
-struct SideCtx {
-    hipStream_t side;
-    hipEvent_t fork, join;
-};
-
-
-static int side_ctx(hipStream_t main, int dev, SideCtx *out)
+// k_post<MS(S), NPF, RO, JL> (see k_post)
+template <int MS, bool RO, bool JL>
+static void launch_post(const KCfg &k, const KArgs &a, int npf, dim3 grid, int lds, hipStream_t s)
 {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, SideCtx> ctx;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = ctx.find({dev, main});
-    if (it == ctx.end()) {
-        SideCtx c;
-        if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&c.fork, kJoinFlags) != hipSuccess ||
-            hipEventCreateWithFlags(&c.join, kJoinFlags) != hipSuccess) {
-            set_error("side stream / event creation failed");
-            return SNAKE_E_LAUNCH;
-        }
-        it = ctx.emplace(std::make_pair(dev, main), c).first;
-    }
-    *out = it->second;
-    return SNAKE_OK;
+    const dim3 block(kWave);
+    if (npf == 0) hipLaunchKernelGGL((k_post<MS, 0, RO, JL>), grid, block, lds, s, a);
+    else if (npf == 1) hipLaunchKernelGGL((k_post<MS, 1, RO, JL>), grid, block, lds, s, a);
+    else if (npf == 2) hipLaunchKernelGGL((k_post<MS, 2, RO, JL>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((k_post<MS, 8, RO, JL>), grid, block, lds, s, a);
 }
 
-// k_autoreset<MS(S), SLICE, RO, JL(k.link_in_lds)>
-template <bool SLICE, bool RO>
-static void launch_autoreset(const KCfg &k, const KArgs &a, dim3 grid, hipStream_t s)
+template <bool RO, bool JL>
+static void launch_post_s(const KCfg &k, const KArgs &a, int npf, dim3 grid, int lds, hipStream_t s)
+{
+    if (k.S <= 4) launch_post<4, RO, JL>(k, a, npf, grid, lds, s);
+    else if (k.S <= 8) launch_post<8, RO, JL>(k, a, npf, grid, lds, s);
+    else launch_post<16, RO, JL>(k, a, npf, grid, lds, s);
+}
+
+// k_autoreset<MS(S), RO, JL(k.link_in_lds)> (every-step mode: resets only)
+static void launch_autoreset_ro(const KCfg &k, const KArgs &a, dim3 grid, hipStream_t s)
 {
     const dim3 block(kWave);
     if (k.link_in_lds) {
-        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, SLICE, RO, true>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, SLICE, RO, true>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_autoreset<16, SLICE, RO, true>), grid, block, k.lds_bytes, s, a);
-    } else if constexpr (!SLICE) {   // (sliced attempts exist only with the LDS record)
-        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, false, RO, false>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, false, RO, false>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_autoreset<16, false, RO, false>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true, true>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true, true>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_autoreset<16, true, true>), grid, block, k.lds_bytes, s, a);
+    } else {
+        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true, false>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true, false>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_autoreset<16, true, false>), grid, block, k.lds_bytes, s, a);
     }
 }
 
+// snake_step: k_logic, then (all-done auto-reset) the shared phase as ONE launch
+// on the caller's stream -- k_post, or k_post_lean on boards with four-wave lean
+// encodes -- with, on background spawn-ahead boards, k_spawn forked onto the
+// state's background stream after k_logic and not joined.
 int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, const snake_out &o,
                 void *stream)
 {
@@ -2727,6 +2542,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     const int ms = k.logic_ms, epw = kWave / ms;   // envs per k_logic wave
     const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits + epw * ms * kRespawnT * 4 + epw * ms * 2;
     const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
+    // everything that can fail before k_logic fills this step's queue set
     BgCtx *bgc = nullptr;
     if (k.bg) {   // background spawn-ahead: this step's queue set, once the
                   // spawn kernel of two steps ago has read it
@@ -2745,12 +2561,21 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;
+    // From here on k_logic has filled this step's queue set: a failure zeroes
+    // its counters, so the next step does not run this step's queues.
+    auto fail = [&](int r) {
+        int *qc = st.resetq + (int64_t)k.qpar * (kNumQ * kQShards * k.q_cap + kQCounters) +
+                  kNumQ * kQShards * k.q_cap;
+        (void)hipMemsetAsync(qc, 0, sizeof(int) * kQCounters, sm);
+        return r;
+    };
+    const KArgs a{k, st, o, nullptr};
     if (k.autoreset == 2) {   // every env resets (the resets write the obs), then the
                               // encodes of the envs rejected for an invalid action
         TimedLaunch t2("k_autoreset", sm);
-        launch_autoreset<false, true>(k, KArgs{k, st, o, nullptr}, gr, sm);
+        launch_autoreset_ro(k, a, gr, sm);
         t2.close();
-        if ((rc = check_launch("k_autoreset"))) return rc;
+        if ((rc = check_launch("k_autoreset"))) return fail(rc);
         TimedLaunch t3("k_encode", sm);
         hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
         t3.close();
@@ -2762,13 +2587,12 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         t3.close();
         return check_launch("k_encode");
     }
-    // this step's spawn kernel (background spawn-ahead) on the background
-    // stream once `fork` (recorded on the caller's stream after k_logic) has
-    // passed; not joined
-    auto launch_spawn = [&](hipEvent_t fork) -> int {
-        if (hipStreamWaitEvent(bgc->x, fork, 0) != hipSuccess) {
-            set_error("ordering the background spawn kernel failed");
-            return SNAKE_E_LAUNCH;
+    if (bgc) {
+        // this step's spawn kernel on the background stream once k_logic has
+        // passed; not joined (the k_logic two steps later waits for it)
+        if (hipEventRecord(bgc->fork, sm) != hipSuccess || hipStreamWaitEvent(bgc->x, bgc->fork, 0) != hipSuccess) {
+            set_error("fork to the background stream failed");
+            return fail(SNAKE_E_LAUNCH);
         }
         KCfg ks = k;
         ks.lds_link = 0;   // (only the draw record)
@@ -2780,123 +2604,42 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         else if (k.S <= 8) hipLaunchKernelGGL(k_spawn<8>, gs, block, lds_sp, bgc->x, sa);
         else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bgc->x, sa);
         t4.close();
-        if (int rc2 = check_launch("k_spawn")) return rc2;
+        if ((rc = check_launch("k_spawn"))) return fail(rc);
         if (hipEventRecord(bgc->done[k.qpar], bgc->x) != hipSuccess) {
             set_error("background spawn event failed");
-            return SNAKE_E_LAUNCH;
+            return fail(SNAKE_E_LAUNCH);
         }
         bgc->pending[k.qpar] = true;
         bgc->steps++;
-        return SNAKE_OK;
-    };
-    SideCtx sc;
-    if ((rc = side_ctx(sm, dg.dev, &sc))) return rc;
-    if (k.post_lean && bgc && st.jscratch && k.lean && k.lean_threads == 256 && k.autoreset == 1) {
-        // one launch: four resets-only workers per workgroup, then the lean
-        // encodes (k_post_lean); the spawn kernel forks off after k_logic
-        if (hipEventRecord(sc.fork, sm) != hipSuccess) {
-            set_error("fork to the background stream failed");
-            return SNAKE_E_LAUNCH;
-        }
-        if ((rc = launch_spawn(sc.fork))) return rc;
-        const int epw2 = k.enc_per_wave;
-        const dim3 gp((k.reset_slots + 3) / 4 + (k.N + epw2 - 1) / epw2);
-        const int lds_p = std::max(4 * k.lds_worker, k.lds_lean_bytes);
-        const KArgs a{k, st, o, nullptr};
-        TimedLaunch t2("k_post", sm);
-        if (k.S <= 4) hipLaunchKernelGGL(k_post_lean<4>, gp, dim3(256), lds_p, sm, a);
-        else if (k.S <= 8) hipLaunchKernelGGL(k_post_lean<8>, gp, dim3(256), lds_p, sm, a);
-        else hipLaunchKernelGGL(k_post_lean<16>, gp, dim3(256), lds_p, sm, a);
-        t2.close();
-        return check_launch("k_post_lean");
     }
-    if (k.fused && !k.spawn_budget && k.link_in_lds && !k.lean) {
-        // one launch on the caller's stream: workers, then encodes (k_post);
-        // with background spawn-ahead the workers run the resets only (RO)
-        if (bgc) {
-            if (hipEventRecord(sc.fork, sm) != hipSuccess) {
-                set_error("fork to the background stream failed");
-                return SNAKE_E_LAUNCH;
-            }
-            if ((rc = launch_spawn(sc.fork))) return rc;
+    TimedLaunch t2("k_post", sm);
+    if (k.lean) {
+        // four workers per workgroup, then the four-wave lean encodes
+        const dim3 gp((k.reset_slots + 3) / 4 + (k.N + k.enc_per_wave - 1) / k.enc_per_wave);
+        const int lds_p = std::max(4 * k.lds_worker, k.lds_lean_bytes);
+        if (k.bg) {
+            if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, true>), gp, dim3(256), lds_p, sm, a);
+            else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, true>), gp, dim3(256), lds_p, sm, a);
+            else hipLaunchKernelGGL((k_post_lean<16, true>), gp, dim3(256), lds_p, sm, a);
+        } else {
+            if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, false>), gp, dim3(256), lds_p, sm, a);
+            else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, false>), gp, dim3(256), lds_p, sm, a);
+            else hipLaunchKernelGGL((k_post_lean<16, false>), gp, dim3(256), lds_p, sm, a);
         }
+    } else {
+        // the workers, then the encodes: NPF = 16-byte ring chunks per lane the
+        // two-env encode keeps in flight, 0 = one env per block
         const int epw2 = k.enc_per_wave, n16 = k.ring_bytes >> 4;
         const int npf = epw2 <= 1 ? 0 : (n16 <= kWave ? 1 : (n16 <= 2 * kWave ? 2 : 8));
         const int enc_blocks = npf == 0 ? k.N : (k.N + epw2 - 1) / epw2;
         const dim3 gp(k.reset_slots + enc_blocks);
         const int lds_p = std::max(k.lds_bytes, k.lds_obs_bytes);
-        const KArgs a{k, st, o, nullptr};
-        TimedLaunch t2("k_post", sm);
-#define SNAKE_POST(MS_, RO_)                                                                          \
-        do {                                                                                          \
-            if (npf == 0) hipLaunchKernelGGL((k_post<MS_, 0, RO_>), gp, block, lds_p, sm, a);         \
-            else if (npf == 1) hipLaunchKernelGGL((k_post<MS_, 1, RO_>), gp, block, lds_p, sm, a);    \
-            else if (npf == 2) hipLaunchKernelGGL((k_post<MS_, 2, RO_>), gp, block, lds_p, sm, a);    \
-            else hipLaunchKernelGGL((k_post<MS_, 8, RO_>), gp, block, lds_p, sm, a);                  \
-        } while (0)
-        if (k.bg) {
-            if (k.S <= 4) SNAKE_POST(4, true);
-            else if (k.S <= 8) SNAKE_POST(8, true);
-            else SNAKE_POST(16, true);
-        } else {
-            if (k.S <= 4) SNAKE_POST(4, false);
-            else if (k.S <= 8) SNAKE_POST(8, false);
-            else SNAKE_POST(16, false);
-        }
-#undef SNAKE_POST
-        t2.close();
-        return check_launch("k_post");
+        if (k.bg) launch_post_s<true, true>(k, a, npf, gp, lds_p, sm);   // (background boards keep the LDS record)
+        else if (k.link_in_lds) launch_post_s<false, true>(k, a, npf, gp, lds_p, sm);
+        else launch_post_s<false, false>(k, a, npf, gp, lds_p, sm);
     }
-    // fork: the resets and spawn-ahead jobs go first on the caller's stream
-    // (dispatched the moment k_logic retires: dispatched second, behind the
-    // encodes' 64K waves, they would wait for LDS), the encodes follow on the
-    // side stream; join before return. SNAKE_ENCODE_ON_MAIN=1 swaps the two
-    // (A/B probe: 0.155 vs 0.135 ms per step for cfg3).
-    if (hipEventRecord(sc.fork, sm) != hipSuccess || hipStreamWaitEvent(sc.side, sc.fork, 0) != hipSuccess) {
-        set_error("fork to the side stream failed");
-        return SNAKE_E_LAUNCH;
-    }
-    if (bgc && (rc = launch_spawn(sc.fork))) return rc;
-    static const bool resets_main = !(getenv("SNAKE_ENCODE_ON_MAIN") && atoi(getenv("SNAKE_ENCODE_ON_MAIN")));
-    const hipStream_t s_res = resets_main ? sm : sc.side, s_enc = resets_main ? sc.side : sm;
-    auto launch_resets = [&]() {
-        TimedLaunch t2("k_autoreset", s_res);
-        // (the sliced form only where a time slice is set: its pause bookkeeping
-        // costs registers in every job)
-        const KArgs a{k, st, o, nullptr};
-        if (k.spawn_budget && k.link_in_lds) launch_autoreset<true, false>(k, a, gr, s_res);
-        else if (k.bg) launch_autoreset<false, true>(k, a, gr, s_res);
-        else launch_autoreset<false, false>(k, a, gr, s_res);
-        t2.close();
-        return check_launch("k_autoreset");
-    };
-    auto launch_encode = [&]() {
-        TimedLaunch t3("k_encode", s_enc);
-        const int epw2 = k.enc_per_wave;
-        const int lds_enc = k.lean ? k.lds_lean_bytes : k.lds_obs_bytes;
-        const dim3 ge((k.N + epw2 - 1) / epw2);
-        const int n16 = k.ring_bytes >> 4;
-        const int npw = (k.fs * k.HW / 4 + k.lean_threads - 1) / k.lean_threads;   // frame dwords per thread (lean)
-        if (k.lean && k.lean_threads == 256) hipLaunchKernelGGL((k_encode_lean<8, 256>), ge, dim3(256), lds_enc, s_enc, k, st, o);
-        else if (k.lean && npw <= 2) hipLaunchKernelGGL((k_encode_lean<2, kWave>), ge, block, lds_enc, s_enc, k, st, o);
-        else if (k.lean && npw <= 8) hipLaunchKernelGGL((k_encode_lean<8, kWave>), ge, block, lds_enc, s_enc, k, st, o);
-        else if (k.lean) hipLaunchKernelGGL((k_encode_lean<32, kWave>), ge, block, lds_enc, s_enc, k, st, o);
-        else if (epw2 <= 1) hipLaunchKernelGGL(k_encode, g1, block, lds_enc, s_enc, k, st, o);
-        else if (n16 <= kWave) hipLaunchKernelGGL(k_encode_multi<1>, ge, block, lds_enc, s_enc, k, st, o);
-        else if (n16 <= 2 * kWave) hipLaunchKernelGGL(k_encode_multi<2>, ge, block, lds_enc, s_enc, k, st, o);
-        else hipLaunchKernelGGL(k_encode_multi<8>, ge, block, lds_enc, s_enc, k, st, o);
-        t3.close();
-        return check_launch("k_encode");
-    };
-    if (resets_main) {
-        if ((rc = launch_resets()) || (rc = launch_encode())) return rc;
-    } else {
-        if ((rc = launch_encode()) || (rc = launch_resets())) return rc;
-    }
-    if (hipEventRecord(sc.join, sc.side) != hipSuccess || hipStreamWaitEvent(sm, sc.join, 0) != hipSuccess) {
-        set_error("join from the side stream failed");
-        return SNAKE_E_LAUNCH;
-    }
+    t2.close();
+    if ((rc = check_launch("k_post"))) return fail(rc);
     return SNAKE_OK;
 }
 
@@ -2915,11 +2658,13 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
         snake::set_error("snake_timing_read: NULL argument");
         return SNAKE_E_ARG;
     }
+    const bool one = !strcmp(kernel, "resets") || !strcmp(kernel, "resets_timed");
     const void *sym = !strcmp(kernel, "resets") ? (const void *)&snake::g_resets_run
+                    : !strcmp(kernel, "resets_timed") ? (const void *)&snake::g_resets_timed
                     : !strcmp(kernel, "spawn_hits") ? (const void *)snake::g_spawn_hits
                     : !strcmp(kernel, "spawn_jobs") ? (const void *)snake::g_spawn_jobs : nullptr;
     if (sym) {
-        const int n = sym == (const void *)&snake::g_resets_run ? 1 : snake::kDiagSlots * snake::kDiagSpread;
+        const int n = one ? 1 : snake::kDiagSlots * snake::kDiagSpread;
         std::vector<unsigned long long> v(n, 0ull), z(n, 0ull);
         if (hipMemcpyFromSymbol(v.data(), sym, n * sizeof(unsigned long long)) != hipSuccess ||
             hipMemcpyToSymbol(sym, z.data(), n * sizeof(unsigned long long)) != hipSuccess) {
@@ -2953,7 +2698,7 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
     return SNAKE_OK;
 }
 
-#if defined(SNAKE_STAMPS) || defined(SNAKE_DRAWBENCH)
+#ifdef SNAKE_DRAWBENCH
 // Isolated draw benchmark: one permutation's draws on one wave, outside the
 // reset kernel's register pressure (cycles, final MT position).
 __global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsigned long long *out)
@@ -2985,23 +2730,11 @@ extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, in
 #endif
 
 #ifdef SNAKE_STAMPS
-extern "C" int snake_debug_obsprof(unsigned long long *out /* 1408 */)
+// out: 64 phase stamps of block 0, then 2 * 8192 wave start/end realtimes
+extern "C" int snake_debug_stamps(unsigned long long *out)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_obsprof), sizeof(unsigned long long) * 1408) != hipSuccess)
-        return -1;
-    unsigned long long z[1408] = {0};
-    hipMemcpyToSymbol(HIP_SYMBOL(snake::g_obsprof), z, sizeof z);
-    return 0;
-}
-
-extern "C" int snake_debug_stamps(unsigned long long *out /* 72 */)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_stamps), sizeof(unsigned long long) * 64) != hipSuccess)
-        return -1;
-    if (hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(snake::g_counts), sizeof(unsigned long long) * 8) != hipSuccess)
-        return -1;
-    unsigned long long z[8] = {0};
-    hipMemcpyToSymbol(HIP_SYMBOL(snake::g_counts), z, sizeof z);
-    return 0;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_stamps), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(snake::g_wavetime),
+                               sizeof(unsigned long long) * 2 * snake::kWaveTimes) == hipSuccess ? 0 : -1;
 }
 #endif

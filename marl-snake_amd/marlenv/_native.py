@@ -10,11 +10,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 13
+SNAKE_ABI_VERSION = 14
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
-           'snake_sync', 'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version',
+           'snake_sync', 'snake_release', 'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version',
            'snake_dqn_plan', 'snake_dqn_rows', 'snake_dqn_forward', 'snake_dqn32_scratch', 'snake_dqn32_forward')
 
 
@@ -27,12 +27,12 @@ class SnakeCfg(ctypes.Structure):
                 ('rew_lose', ctypes.c_double), ('rew_win', ctypes.c_double),
                 ('rew_time', ctypes.c_double), ('max_episode_steps', ctypes.c_double),
                 ('coop', ctypes.c_int32), ('autoreset', ctypes.c_int32), ('spawn_ahead', ctypes.c_int32),
-                ('spawn_budget_us', ctypes.c_int32), ('spawn_background', ctypes.c_int32)]
+                ('spawn_background', ctypes.c_int32)]
 
 
 class SnakeLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
-        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'spawn', 'spawn_draws', 'resetq',
+        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'spawn', 'resetq',
         'obs', 'rew',
         'done',
         'ep_done', 'rank', 'ep_stats', 'err', 'n_cand')] + [
@@ -42,7 +42,7 @@ class SnakeLayout(ctypes.Structure):
 
 class SnakeState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
-        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'spawn', 'spawn_draws', 'resetq')]
+        'grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt', 'cand', 'jscratch', 'spawn', 'resetq')]
 
 
 class SnakeOut(ctypes.Structure):
@@ -107,6 +107,7 @@ def lib(path=None):
     L.snake_step.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P,
                              ctypes.POINTER(SnakeOut), P]
     L.snake_sync.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P]
+    L.snake_release.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64]
     L.snake_render_rgb.argtypes = [ctypes.POINTER(SnakeCfg), ctypes.POINTER(SnakeState), I64, P, P, P]
     L.snake_dqn_plan.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(DqnLayout)]
     L.snake_dqn_rows.argtypes = [ctypes.POINTER(DqnCfg), P, I64]
@@ -130,7 +131,7 @@ def timing_enable(on, L=None):
 
 def timing_read(kernel, L=None):
     """(total device ms, launches) of one kernel since its last read; for
-    kernel='resets' the auto-reset count (ms is 0)."""
+    kernel='resets' / 'resets_timed' / 'spawn_hits' / 'spawn_jobs' a count (ms is 0)."""
     L = L or lib()
     ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
     check(L.snake_timing_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)), L)

@@ -39,8 +39,6 @@ def build_cfg(height=20, width=20, num_snakes=4, snake_length=3, vision_range=No
     max_episode_steps = kwargs.pop('max_episode_steps', MAX_EPISODE_STEPS)
     # spawn-ahead threshold of the GPU step (include/snake_env.h; 0 default, -1 off)
     spawn_ahead = int(kwargs.pop('spawn_ahead', 0))
-    # time slice of the spawn-ahead attempts per step, us (0 automatic, -1 unlimited)
-    spawn_budget_us = int(kwargs.pop('spawn_budget_us', 0))
     # spawn-ahead attempts in a background kernel (0 automatic, 1 on, -1 off)
     spawn_background = int(kwargs.pop('spawn_background', 0))
     num_fruits = kwargs.pop('num_fruits', int(round(num_snakes * 0.8)))
@@ -51,7 +49,7 @@ def build_cfg(height=20, width=20, num_snakes=4, snake_length=3, vision_range=No
         int(frame_stack), 1 if observer == 'human' else 0, int(num_fruits),
         float(reward_dict['fruit']), float(reward_dict['kill']), float(reward_dict['lose']),
         float(reward_dict['win']), float(reward_dict['time']), float(max_episode_steps),
-        1 if coop else 0, autoreset_code(autoreset), spawn_ahead, spawn_budget_us, spawn_background)
+        1 if coop else 0, autoreset_code(autoreset), spawn_ahead, spawn_background)
     meta = dict(height=int(height), width=int(width), num_snakes=int(num_snakes),
                 snake_length=int(snake_length), vision_range=vision_range,
                 frame_stack=int(frame_stack), observer=observer, reward_dict=reward_dict,

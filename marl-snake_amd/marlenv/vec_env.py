@@ -54,12 +54,15 @@ _INFO_KEYS = ('episode_done', 'rank', 'episode_scores', 'episode_steps', 'episod
 
 class _StepInfo(dict):
     """info of one SnakeVecEnv.step: a dict whose tensors are views of the step's
-    output slab, made when first read (most callers never read most of them)."""
-    __slots__ = ('_env', '_slab', '_es')
+    output slab, made when first read (most callers never read most of them).
+    The fills run on the stream the step was enqueued on (its raw handle,
+    `_stream`), whatever stream is current at the read; pickling / deepcopy give
+    a plain dict of the tensors."""
+    __slots__ = ('_env', '_slab', '_es', '_stream')
 
-    def __init__(self, env, slab):
+    def __init__(self, env, slab, stream):
         dict.__init__(self, dict.fromkeys(_INFO_KEYS))
-        self._env, self._slab, self._es = env, slab, None
+        self._env, self._slab, self._es, self._stream = env, slab, None, stream
 
     def _make(self, k):
         # rank / ep_stats are stored only where the episode ended (include/snake_env.h
@@ -70,10 +73,18 @@ class _StepInfo(dict):
         if k == 'error':
             return env._view(slab, 'err')
         ended = self['episode_done'].view(-1, 1)
-        if k == 'rank':
-            return env._view(slab, 'rank').masked_fill(~ended, 0)
-        if self._es is None:
-            self._es = env._view(slab, 'ep_stats').masked_fill(~ended.view(-1, 1, 1), 0.0)
+        torch = _torch()
+        if _raw_stream(env._dev_index) == self._stream:
+            ctx = torch.cuda.device(env.device)           # (already the step's stream)
+        else:
+            st = (torch.cuda.default_stream(env.device) if not self._stream
+                  else torch.cuda.ExternalStream(self._stream, device=env.device))
+            ctx = torch.cuda.stream(st)
+        with ctx:
+            if k == 'rank':
+                return env._view(slab, 'rank').masked_fill(~ended, 0)
+            if self._es is None:
+                self._es = env._view(slab, 'ep_stats').masked_fill(~ended.view(-1, 1, 1), 0.0)
         return self._es[:, ('episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills').index(k)]
 
     def __getitem__(self, k):
@@ -82,6 +93,13 @@ class _StepInfo(dict):
             v = self._make(k)
             dict.__setitem__(self, k, v)
         return v
+
+    def __reduce__(self):
+        return (dict, (self.copy(),))
+
+    def __deepcopy__(self, memo):
+        import copy
+        return copy.deepcopy(self.copy(), memo)
 
     def get(self, k, default=None):
         return self[k] if k in self else default
@@ -144,9 +162,6 @@ class SnakeVecEnv:
         self.mt = buf(lay.mt, torch.int32)
         self.jscratch = buf(lay.jscratch, torch.int32) if lay.jscratch else None
         self.spawn = buf(lay.spawn, torch.int32)
-        # draws of paused spawn-ahead attempts: written before they are read, no zero fill
-        self.spawn_draws = (torch.empty(int(lay.spawn_draws) // 2, dtype=torch.int16, device=dev)
-                            if lay.spawn_draws else None)
         self.resetq = buf(lay.resetq, torch.int32)
         cap = int(lay.n_cand) * self.cfg.snake_length
         host = np.zeros(cap, np.int16)
@@ -157,8 +172,7 @@ class SnakeVecEnv:
             self.grid.data_ptr(), self.snake.data_ptr(), self.body.data_ptr(), self.env_rec.data_ptr(),
             self.ctr.data_ptr(), self.stats.data_ptr(), self.mt.data_ptr(), self.cand.data_ptr(),
             self.jscratch.data_ptr() if self.jscratch is not None else None,
-            self.spawn.data_ptr(), self.spawn_draws.data_ptr() if self.spawn_draws is not None else None,
-            self.resetq.data_ptr())
+            self.spawn.data_ptr(), self.resetq.data_ptr())
         with torch.cuda.device(dev):
             check(L.snake_seed(ctypes.byref(self.cfg), ctypes.byref(self._state), N, self.seed_base,
                                self.env_offset, self._stream()))
@@ -302,7 +316,7 @@ class SnakeVecEnv:
         if rc < 0:
             check(rc, self._L)
         self._keep = a
-        info = _StepInfo(self, slab)
+        info = _StepInfo(self, slab, stream)
         if self.strict and bool(info['error'].any()):
             err = info['error']
             bad = (err == 1).nonzero().flatten().tolist()
@@ -363,11 +377,6 @@ class SnakeVecEnv:
         self.sync()
         torch.cuda.current_stream(self.device).synchronize()
         sd = {k: getattr(self, k).detach().to(dev, copy=True) for k in self._STATE_BUFFERS}
-        # a paused spawn-ahead attempt keeps its draws in spawn_draws, which is not
-        # saved: the snapshot marks it as no record (spawn-ahead never changes
-        # results, the attempt is simply redone)
-        er = sd['env_rec'].view(self.num_envs, 8)
-        er[:, 4].masked_fill_((er[:, 4] & 3) == 3, 0)
         sd['meta'] = self._snapshot_meta()
         return sd
 
@@ -375,7 +384,7 @@ class SnakeVecEnv:
         lay = self.layout
         return dict(abi=int(self._L.snake_abi_version()), num_envs=self.num_envs,
                     cfg=[getattr(self.cfg, f) for f, _ in self.cfg._fields_
-                         if f not in ('spawn_ahead', 'spawn_budget_us')],
+                         if f != 'spawn_ahead'],
                     sizes=[int(getattr(lay, k)) for k in ('grid', 'snake', 'body', 'env', 'ctr', 'stats',
                                                           'mt', 'spawn')],
                     seed=self.seed_base, env_offset=self.env_offset, reset_done=self._reset_done)
@@ -472,12 +481,15 @@ class SnakeVecEnv:
 
     def close(self):
         # the state buffers go back to the allocator on the current stream: order
-        # that after a background spawn kernel still writing them
+        # that after a background spawn kernel still writing them, then release
+        # the library's background stream and events for this state (snake_release)
         if getattr(self, '_state', None) is not None and torch_cuda_alive():
             try:
                 self.sync()
+                self._L.snake_release(ctypes.byref(self.cfg), ctypes.byref(self._state), self.num_envs)
             except Exception:
                 pass
+            self._state = None
 
     def __del__(self):
         self.close()

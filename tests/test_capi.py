@@ -68,19 +68,16 @@ def test_plan_sizes(native):
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay2)) == 0
     assert lay2.n_cand == 20168 and lay2.jscratch == 2048 * (20168 + 64) * 4   # global link tables
     assert lay.grid == 8192 * 4 * 1600
-    # paused spawn-ahead attempts: u16 per draw index per env where attempts are
-    # sliced (an explicit spawn_budget_us; LDS draw record, spawn-ahead on),
-    # none otherwise
-    assert lay.spawn_draws == 0                                   # 40x40: not sliced by default
-    assert lay2.spawn_draws == 0                                  # global link tables: not sliced
-    for kw in (dict(autoreset=False), dict(autoreset='every_step'), dict(spawn_ahead=-1), {},
-               dict(spawn_budget_us=-1)):
-        c = cfg(native, height=20, width=20, num_snakes=4, **kw)
+    # every-step / no auto-reset: the 40x40 four-frame board needs no worker link tables
+    for kw in (dict(autoreset=False), dict(autoreset='every_step')):
+        c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4, **kw)
         assert native.lib().snake_plan(ctypes.byref(c), 64, ctypes.byref(lay)) == 0
-        assert lay.spawn_draws == 0, kw
-    c = cfg(native, height=20, width=20, num_snakes=4, spawn_budget_us=20)
+        assert lay.jscratch == 0 and lay.spawn == 64 * 656 * 4, kw
+    # in-step spawn-ahead on that board (spawn_background=-1): one record per env,
+    # the k_post_lean workers' link tables
+    c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4, spawn_background=-1)
     assert native.lib().snake_plan(ctypes.byref(c), 64, ctypes.byref(lay)) == 0
-    assert lay.spawn_draws == 64 * 3464 * 2
+    assert lay.jscratch == 64 * (16424 + 64) * 4 and lay.spawn == 64 * 656 * 4
 
 
 @pytest.mark.parametrize('kw,msg', [
