@@ -250,7 +250,7 @@ def main():
 
     L = _native.lib()
     for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_post', 'k_spawn', 'resets', 'resets_timed', 'spawn_hits',
-              'spawn_jobs'):
+              'spawn_jobs', 'spawn_void'):
         _native.timing_read(k, L)                      # drop anything from the warmup
     stride = args.timing_stride if args.timing_stride is not None else max(1, min(32, args.steps // 4))
     if distributed:
@@ -284,6 +284,7 @@ def main():
     resets_t = _native.timing_read('resets_timed', L)[1]
     sp_hits = _native.timing_read('spawn_hits', L)[1]
     sp_jobs = _native.timing_read('spawn_jobs', L)[1]
+    sp_void = _native.timing_read('spawn_void', L)[1]
     # per launch on the event-timed steps (all steps when no step is timed)
     rps_t = resets_t / n_timed if n_timed else resets / args.steps
 
@@ -349,6 +350,8 @@ def main():
                    f'post-reset transient (steps {args.warmup}-{args.warmup + args.steps} after env.reset())'),
         'spawn_ahead': ({'hits_per_step': round(sp_hits / n_timed, 1),
                          'jobs_per_step': round(sp_jobs / n_timed, 1),
+                         'jobs_per_served_reset': round(sp_jobs / max(sp_hits, 1), 3),
+                         'ready_voided_per_step': round(sp_void / n_timed, 1),
                          'hit_rate': round(sp_hits / max(resets_t, 1), 4)}
                         if n_timed else None),
         'cpu_baseline': None,

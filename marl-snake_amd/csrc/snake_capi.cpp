@@ -281,6 +281,7 @@ static bool bg_of(const snake_cfg *c, int64_t n_cand)
 struct LeanGeom {
     int lean, lp, pw, pframe, lds_lean_bytes, ups, rowl;
     uint32_t mag_ups, mag_rowl, mag_fs, mag_wpr;
+    int exact;   // every reciprocal exact, W % 4 == 0, an even unit count: the image and unit maps apply
 };
 
 static LeanGeom lean_geom(const snake_cfg *c)
@@ -299,8 +300,7 @@ static LeanGeom lean_geom(const snake_cfg *c)
     g.mag_wpr = mag(std::max(1, W / 4));
     g.lds_lean_bytes = (int)round_up((int64_t)fs * g.pframe, 16) + 4 * fs * kMaxSnakes;
     const int64_t fdw = (int64_t)fs * H * W / 4;
-    bool ok = fdw > 8 * kWave && fdw <= 8 * 256 && (units % 2) == 0 && units < (1 << 22) &&
-              g.lds_lean_bytes <= 48 * 1024 && W % 4 == 0;
+    bool ok = (units % 2) == 0 && units < (1 << 22) && W % 4 == 0;
     for (int64_t u = 0; ok && u < units; u++) {
         const int64_t q = ((uint64_t)u * g.mag_ups) >> 32, r0 = u - q * g.ups;
         const int64_t i = ((uint64_t)r0 * g.mag_rowl) >> 32, r1 = r0 - i * g.rowl;
@@ -309,7 +309,8 @@ static LeanGeom lean_geom(const snake_cfg *c)
     }
     for (int64_t x = 0; ok && x < (int64_t)H * W / 4; x++)
         ok = (W / 4 == 1 ? x : (int64_t)(((uint64_t)x * g.mag_wpr) >> 32)) == x / (W / 4);
-    g.lean = ok ? 1 : 0;
+    g.exact = ok ? 1 : 0;
+    g.lean = ok && fdw > 8 * kWave && fdw <= 8 * 256 && g.lds_lean_bytes <= 48 * 1024 ? 1 : 0;
     return g;
 }
 
@@ -480,12 +481,28 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         k->lean = g.lean; k->lp = g.lp; k->pw = g.pw; k->pframe = g.pframe;
         k->lds_lean_bytes = g.lds_lean_bytes; k->ups = g.ups; k->rowl = g.rowl;
         k->mag_ups = g.mag_ups; k->mag_rowl = g.mag_rowl; k->mag_fs = g.mag_fs; k->mag_wpr = g.mag_wpr;
+        // the table encode (snake_kernels.hip encode_tbl_block) where k_post runs
+        // the encodes: rings of at most 512 dwords, the lean geometry exact
+#ifndef SNAKE_ENC_TBL
+#define SNAKE_ENC_TBL 1
+#endif
+        const int64_t fdw = (int64_t)k->fs * k->HW / 4;
+        int t = 0;
+        k->tbl_base = (int)round_up((int64_t)k->fs * k->pframe, 16); t = k->tbl_base + 8 * k->fs * kMaxSnakes;
+        k->tbl_pat = t; t += 8 * k->S * 160;   // (kPatV)
+        k->tbl_desc = t; t += (int)round_up(4 * (int64_t)k->units, 16);
+        k->lds_tbl_bytes = t;
+        k->tbl = SNAKE_ENC_TBL && g.exact && !g.lean && fdw <= 8 * kWave && t <= 40 * 1024 ? 1 : 0;
     }
     // envs per encode wave (k_post's encodes: the next env's ring prefetched into
     // registers, at most 8 16-byte chunks per lane): two at 16 384 envs and more
     // (cfg3 0.1033 -> 0.0998 ms; 4, 8, 16, 32 measured 0.1016, 0.106, 0.114,
     // 0.135), one below (cfg2 0.0622 vs 0.0625); the lean encode two per workgroup
     k->enc_per_wave = k->lean ? 2 : (N >= 16384 && k->ring_bytes <= 8 * 1024 ? 2 : 1);
+#ifndef SNAKE_TBL_EPW
+#define SNAKE_TBL_EPW 4
+#endif
+    if (k->tbl) k->enc_per_wave = SNAKE_TBL_EPW;   // (the tables are built once per wave)
     // the reset workers never use the encode staging buffer: the draw record
     // overlays it (the workers' LDS is what k_encode's waves share the CUs with)
     k->lds_link = k->lds_stage;

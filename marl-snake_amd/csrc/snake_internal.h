@@ -87,6 +87,10 @@ struct KCfg {
     // so the crop needs no bounds test; unit -> (snake, row, col, frame) by
     // multiply-high reciprocals of ups = oh*ow*fs, rowl = ow*fs, fs, and of W/4
     int lean, lp, pw, pframe, lds_lean_bytes, ups, rowl;
+    // table encode in k_post (encode_tbl_block; the lean geometry above, one
+    // wave per env): its LDS carve -- the image at 0, window origins, patterns,
+    // unit descriptors
+    int tbl, tbl_base, tbl_pat, tbl_desc, lds_tbl_bytes;
     uint32_t mag_ups, mag_rowl, mag_fs, mag_wpr;
     double rf, rk, rl, rw, rt, max_steps;
 };

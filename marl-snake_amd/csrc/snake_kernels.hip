@@ -41,16 +41,25 @@ __device__ unsigned long long g_resets_timed;   // the same, while timing is ena
 // device-scope atomic per job serialised thousands of them on the timed steps)
 constexpr int kDiagSlots = 64, kDiagSpread = 16;
 __device__ unsigned long long g_spawn_hits[kDiagSlots * kDiagSpread];   // auto-resets that found a ready record
-__device__ unsigned long long g_spawn_jobs[kDiagSlots * kDiagSpread];   // spawn-ahead attempts run
+__device__ unsigned long long g_spawn_jobs[kDiagSlots * kDiagSpread];   // spawn-ahead jobs dequeued
+__device__ unsigned long long g_spawn_void[kDiagSlots * kDiagSpread];   // ready records voided by a fruit draw
 #define DIAG_ADD(arr) atomicAdd(&(arr)[(blockIdx.x % kDiagSlots) * kDiagSpread], 1ull)
 
 #ifdef SNAKE_STAMPS
 // Diagnostic build only (scripts/logic_stamps.py): s_memtime stamps of block
 // 0's wave at k_logic's phase boundaries, and s_memrealtime (100 MHz) at every
 // k_logic wave's start and end (its block index, up to kWaveTimes blocks).
-constexpr int kWaveTimes = 8192;
+constexpr int kWaveTimes = 8192, kPostTimes = 40960;
 __device__ unsigned long long g_stamps[64];
 __device__ unsigned long long g_wavetime[2 * kWaveTimes];
+__device__ unsigned long long g_posttime[2 * kPostTimes];   // k_post: every block's start and end
+#define PTIME(end)                                                                 \
+    do {                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < kPostTimes)                    \
+            g_posttime[2 * blockIdx.x + (end)] = __builtin_amdgcn_s_memrealtime(); \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+    } while (0)
 #define LSTAMP(idx)                                                                \
     do {                                                                           \
         if (blockIdx.x == 0) {                                                     \
@@ -70,6 +79,7 @@ __device__ unsigned long long g_wavetime[2 * kWaveTimes];
 #else
 #define LSTAMP(idx) do {} while (0)
 #define WTIME(end) do {} while (0)
+#define PTIME(end) do {} while (0)
 #endif
 
 enum { C_EMPTY = 0, C_WALL = 1, C_FRUIT = 2, C_HEAD = 3, C_BODY = 4, C_TAIL = 5 };
@@ -164,22 +174,36 @@ __device__ __forceinline__ int bcast(int v, int k) { return __builtin_amdgcn_rea
 // ---- exchanges inside k_logic's env groups of G = 4, 8 or 16 lanes (aligned
 // inside a 16-lane DPP row) by DPP moves, not through the LDS: a __shfl
 // (ds_bpermute) is an LDS round trip on the rules' dependency chain.
+// A DPP move reads its source lane's register only when that lane is active:
+// every move here runs with the whole wave active, and its result passes
+// through an empty volatile asm, so the compiler cannot sink it into a branch
+// that only some lanes take (it did: a select on a DPP result became an
+// exec-masked branch around the move, which then read disabled lanes).
+__device__ __forceinline__ int dpp_pin(int x)
+{
+    __asm__ volatile("" : "+v"(x));
+    return x;
+}
+
 // gsel<G, J>(v): the value of lane J of this lane's group.
 template <int G, int J>
 __device__ __forceinline__ int gsel(int v)
 {
     static_assert(G == 4 || G == 8 || G == 16, "group of 4, 8 or 16 lanes");
+#ifdef SNAKE_NO_DPP
+    return __shfl(v, (int)(threadIdx.x & ~(G - 1)) + J);
+#endif
     if constexpr (G == 4) {
-        return __builtin_amdgcn_mov_dpp(v, J * 0x55, 0xf, 0xf, false);   // quad_perm:[J,J,J,J]
+        return dpp_pin(__builtin_amdgcn_mov_dpp(v, J * 0x55, 0xf, 0xf, false));   // quad_perm:[J,J,J,J]
     } else if constexpr (G == 16) {
-        return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, false);   // row_newbcast:J
+        return dpp_pin(__builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, false));   // row_newbcast:J
     } else {
-        // lane J & 3 of the lane's quad, then, in the group's other quad, that
-        // value moved over by four lanes
-        const int t = __builtin_amdgcn_mov_dpp(v, (J & 3) * 0x55, 0xf, 0xf, false);
-        const bool upper = (threadIdx.x & 4) != 0;
-        if constexpr (J < 4) return upper ? __builtin_amdgcn_mov_dpp(t, 0x114, 0xf, 0xf, false) : t;   // row_shr:4
-        else return upper ? t : __builtin_amdgcn_mov_dpp(t, 0x104, 0xf, 0xf, false);                   // row_shl:4
+        // lane J & 3 of the lane's quad; then the group's other quad (DPP banks
+        // 1, 3 for J < 4, else 0, 2) takes that value from four lanes over,
+        // the bank mask keeping the rest
+        const int t = dpp_pin(__builtin_amdgcn_mov_dpp(v, (J & 3) * 0x55, 0xf, 0xf, false));
+        if constexpr (J < 4) return dpp_pin(__builtin_amdgcn_update_dpp(t, t, 0x114, 0xf, 0xa, false));   // row_shr:4
+        else return dpp_pin(__builtin_amdgcn_update_dpp(t, t, 0x104, 0xf, 0x5, false));                   // row_shl:4
     }
 }
 
@@ -195,10 +219,25 @@ __device__ __forceinline__ double gsel(double v)
 template <int G>
 __device__ __forceinline__ int gscan(int v, int k)
 {
-    v += k >= 1 ? __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false) : 0;   // row_shr:1
-    v += k >= 2 ? __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false) : 0;   // row_shr:2
-    if constexpr (G >= 8) v += k >= 4 ? __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false) : 0;
-    if constexpr (G >= 16) v += k >= 8 ? __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false) : 0;
+#ifdef SNAKE_NO_DPP
+    for (int o = 1; o < G; o <<= 1) {
+        const int n = __shfl_up(v, o);
+        if (k >= o) v += n;
+    }
+    return v;
+#endif
+    int x = dpp_pin(__builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v += k >= 1 ? x : 0;
+    x = dpp_pin(__builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));       // row_shr:2
+    v += k >= 2 ? x : 0;
+    if constexpr (G >= 8) {
+        x = dpp_pin(__builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));
+        v += k >= 4 ? x : 0;
+    }
+    if constexpr (G >= 16) {
+        x = dpp_pin(__builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));
+        v += k >= 8 ? x : 0;
+    }
     return v;
 }
 
@@ -1151,21 +1190,60 @@ __device__ __forceinline__ void stage_to_lds(uint8_t *dst, const uint8_t *src, i
 // frame goes to its ring slot; an env whose episode ended is queued for its
 // auto-reset. The wave-wide parts (dying-body erase, fruit respawn) loop over the
 // block's envs that need them.
+//
+// The round-1 inputs of one group (LogicIn, logic_load): env records, snake
+// records, actions, running statistics; logic_body runs the group. (A
+// persistent form whose waves loaded the next group's inputs, frames
+// included, before running the current one measured slower: cfg3 k_logic 24.4
+// -> 30.6 us at 8 waves per CU, 42.5 at 4 -- the per-wave latency chain, not
+// the loads, sets the kernel's length.)
+struct LogicIn {
+    int4 er, er2, rec;
+    uint4 sv;
+    int act;
+};
+
 template <int MS>
-__global__ void __launch_bounds__(64) k_logic(const KArgs)
+__device__ __forceinline__ void logic_load(const int blk, LogicIn &in)
 {
-    WTIME(0);
+    const KArgs &A = kargs();
+    const KCfg &c = A.c;
+    const snake_state &st = A.st;
+    constexpr int G = MS, E = kWave / MS;
+    const int lane = threadIdx.x, g = lane / G, k = lane - g * G;
+    const int e0 = blk * E, e = e0 + g;
+    const int S = c.S;
+    const bool env_ok = e < c.N;
+    in.er = in.er2 = in.rec = make_int4(0, 0, 0, 0);
+    in.sv = make_uint4(0, 0, 0, 0);
+    in.act = 0;
+    if (env_ok) {
+        in.er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
+        // loaded whatever the threshold: a step run with spawn-ahead off must
+        // still void a record its fruit draws make stale
+        in.er2 = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec + 4);
+    }
+    if (env_ok && k < S) {
+        in.rec = reinterpret_cast<const int4 *>(st.snake)[(int64_t)e * S + k];
+        in.act = reinterpret_cast<const int8_t *>(A.aux)[(int64_t)e * S + k];
+        // the snake's running episode statistics, one 16-byte record (snake_epi_stat)
+        in.sv = reinterpret_cast<const uint4 *>(st.stats)[(int64_t)e * S + k];
+    }
+}
+
+template <int MS>
+__device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
+{
     LSTAMP(40);
     const KArgs &A = kargs();
     const KCfg &c = A.c;
     const snake_state &st = A.st;
     const snake_out &o = A.o;
-    const int8_t *__restrict__ actions = (const int8_t *)A.aux;
     constexpr int G = MS, E = kWave / MS;
     constexpr uint32_t gmask = (1u << G) - 1u;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x, g = lane / G, k = lane - g * G, gb = g * G;
-    const int e0 = blockIdx.x * E, e = e0 + g;
+    const int e0 = blk * E, e = e0 + g;
     const int S = c.S, W = c.W, cap = c.ring_cap, fs = c.fs, stride = c.grid_stride;
     const int n16 = stride >> 4;
     const bool env_ok = e < c.N;
@@ -1182,25 +1260,12 @@ __global__ void __launch_bounds__(64) k_logic(const KArgs)
     int *qcnt = qb + kNumQ * kQShards * c.q_cap;
     auto gbits = [&](unsigned long long m) -> uint32_t { return (uint32_t)(m >> gb) & gmask; };
 
-    // ---- every load this step needs, issued up front
-    int4 er = make_int4(0, 0, 0, 0), er2 = make_int4(0, 0, 0, 0);
-    if (env_ok) {
-        er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
-        // loaded whatever the threshold: a step run with spawn-ahead off must
-        // still void a record its fruit draws make stale
-        er2 = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec + 4);
-    }
+    // ---- the round-1 inputs (logic_load)
+    const int4 er = in.er, er2 = in.er2, rec = in.rec;
+    const uint4 sv = in.sv;
+    const int act = in.act;
     const int spst = er2.x & 3;   // ENV_SPAWN
-    int4 rec = make_int4(0, 0, 0, 0);
-    int act = 0;
-    // the snake's running episode statistics, one 16-byte record (snake_epi_stat)
-    uint4 sv = make_uint4(0, 0, 0, 0);
     uint4 *sp = reinterpret_cast<uint4 *>(st.stats) + (int64_t)e * S + k;
-    if (isn) {
-        rec = reinterpret_cast<const int4 *>(st.snake)[(int64_t)e * S + k];
-        act = actions[(int64_t)e * S + k];
-        sv = *sp;
-    }
     const int alive0 = er.x, eplen = er.y, cur = er.z, mtpos = er.w;
     // stage the E current frames (env g's at lds + g * stride): eight 16-B loads
     // in flight per lane before the LDS writes (a load-wait-write loop pays one
@@ -1621,6 +1686,7 @@ __global__ void __launch_bounds__(64) k_logic(const KArgs)
     // old state (k_spawn) then fails its final compare-and-swap, or, if that landed
     // first, is overwritten here; so with bg every draw writes the word)
     const bool spw_wr = drew && (c.bg || spst != SPAWN_NONE);
+    if (c.diag && drew && spst == SPAWN_READY && k == 0) DIAG_ADD(g_spawn_void);
     const uint32_t spw1 = drew ? (((uint32_t)er2.x >> 3) + 1u) << 3 : (uint32_t)er2.x;
 
     LSTAMP(45);
@@ -1708,8 +1774,18 @@ __global__ void __launch_bounds__(64) k_logic(const KArgs)
         reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + k] = nrec;
     }
     LSTAMP(47);
+}
+
+template <int MS>
+__global__ void __launch_bounds__(64) k_logic(const KArgs)
+{
+    WTIME(0);
+    LogicIn in;
+    logic_load<MS>((int)blockIdx.x, in);
+    logic_body<MS>((int)blockIdx.x, in);
     WTIME(1);
 }
+
 
 // ---------------------------------------------------- step: the observation
 // Two kernels that run concurrently after k_logic (launch_step forks them onto
@@ -2086,9 +2162,124 @@ __device__ __forceinline__ void encode_multi(const KCfg &c, const snake_state &s
 // cfg3 0.0970 -> 0.0941 ms, cfg2 0.0591 -> 0.0539); the kernel's registers and
 // LDS are the larger of the two. JL: the workers' draw record in LDS, else their
 // global link tables (boards of more than 18 368 spawn poses).
+// ---------------------------------------------------------- table encode
+// The observation of c.enc_per_wave consecutive envs per wave (_encode
+// snake_env.py:474-519 + the frame stack :444-472) as table lookups. Per 8-byte
+// unit (snake k, window row i, column j, frame f: obs (S, oh, ow, 8 fs)) the grid
+// byte v of frame f at that window cell comes from a zero-bordered LDS image of
+// the env's frames (no bounds test: cells outside the grid read 0), and the
+// unit's 8 one-hot channels are the table entry pat[k][v] (onehot()). A lane's
+// units are the same for every env: their descriptors desc[u] = (i * pw + j) |
+// (f * 16 + k) << 16 are built once per wave, and per env only the window
+// origins base[f * 16 + k] = (LDS byte of the window origin in frame f, byte
+// offset of pat[k]) change. Per 16-byte store: one descriptor pair, two window
+// origins, two grid bytes and two patterns from LDS, four address adds. The
+// next env's frames (NPW dwords per lane), slot, crop centres and reset flag
+// are loaded into registers during this env's encode (as encode_lean_block).
+constexpr int kPatV = 160;   // grid byte values 10 * id + code (id < 16, code <= 5)
+
+template <int NPW>
+__device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const snake_out &o, const int blk)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    if (c.encode_prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (c.encode_prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (c.encode_prio == 3) __builtin_amdgcn_s_setprio(3);
+    uint8_t *pf = lds;                                                   // fs * pframe bytes
+    uint2 *base = reinterpret_cast<uint2 *>(lds + c.tbl_base);           // [fs][16]
+    uint8_t *pat = lds + c.tbl_pat;                                      // uint2 [S][kPatV]
+    uint32_t *desc = reinterpret_cast<uint32_t *>(lds + c.tbl_desc);     // [units]
+    const int S = c.S, fs = c.fs, fsS = fs * S;
+    const int wpr = c.W >> 2, nw = c.H * wpr, nwt = fs * nw, gsw = c.grid_stride >> 2;
+    // per prefetched dword: ring word index and LDS dword index (clamped: the
+    // lanes past the end repeat the last word, same source, same destination)
+    int src[NPW], dst[NPW];
+#pragma unroll
+    for (int u = 0; u < NPW; u++) {
+        const int x = min(lane + u * kWave, nwt - 1);
+        const int s = x / nw, xx = x - s * nw;
+        const int r = fdiv((uint32_t)xx, c.mag_wpr, wpr), c4 = xx - r * wpr;
+        src[u] = s * gsw + xx;
+        dst[u] = (s * c.pframe + (r + c.vr) * c.pw + c.lp) / 4 + c4;
+    }
+    // once per wave: the zero image, the patterns of the codes that occur (0, 1,
+    // 2 and 10 * id + 3..5 for id < S), the unit descriptors
+    zero_lean<kWave>(c, pf, lane);
+    const int npv = 3 + 3 * S;   // occurring codes per snake
+    for (int x = lane; x < S * npv; x += kWave) {
+        const int k = x / npv, r = x - k * npv;
+        const int v = r < 3 ? r : 10 * ((r - 3) / 3) + 3 + (r - 3) % 3;
+        const unsigned long long b = onehot(v, k);
+        reinterpret_cast<uint2 *>(pat)[k * kPatV + v] = make_uint2((uint32_t)b, (uint32_t)(b >> 32));
+    }
+    for (int u = lane; u < c.units; u += kWave) {
+        const int kk = (int)__umulhi((uint32_t)u, c.mag_ups), r0 = u - kk * c.ups;
+        const int ii = (int)__umulhi((uint32_t)r0, c.mag_rowl), r1 = r0 - ii * c.rowl;
+        const int jj = fdiv((uint32_t)r1, c.mag_fs, fs), ff = r1 - jj * fs;
+        desc[u] = (uint32_t)(ii * c.pw + jj) | ((uint32_t)(ff * kMaxSnakes + kk) << 16);
+    }
+    const int e_begin = blk * c.enc_per_wave, e_end = min(c.N, e_begin + c.enc_per_wave);
+    uint32_t w[NPW];
+    int pcur = 0, pctr = 0, pskip = 0;
+#define SNAKE_TBL_FETCH(EE)                                                                        \
+    do {                                                                                           \
+        const int64_t e_ = (EE);                                                                   \
+        const uint32_t *r32_ = reinterpret_cast<const uint32_t *>(st.grid + e_ * c.ring_bytes);    \
+        _Pragma("unroll") for (int u = 0; u < NPW; u++) w[u] = r32_[src[u]];                       \
+        pcur = st.env[e_ * kEnvRec + ENV_CUR];                                                     \
+        pctr = lane < fsS ? st.ctr[e_ * fsS + lane] : 0;                                           \
+        pskip = c.autoreset ? o.ep_done[e_] : 0;                                                   \
+    } while (0)
+    if (e_begin < e_end) SNAKE_TBL_FETCH(e_begin);
+    const int chunks = c.units >> 1;
+    for (int e = e_begin; e < e_end; e++) {
+        const int cur = pcur, skip = pskip;   // (a reset env's obs is written by its reset)
+        wave_sync();                          // (the previous encode has read the LDS image)
+        if (!skip) {
+#pragma unroll
+            for (int u = 0; u < NPW; u++) reinterpret_cast<uint32_t *>(pf)[dst[u]] = w[u];
+            if (lane < fsS) {
+                // ring slot s = lane / S holds frame f = s - (the oldest slot), mod fs
+                const int s = lane / S, k = lane - s * S, slot0 = cur + 1 == fs ? 0 : cur + 1;
+                const int f = s >= slot0 ? s - slot0 : s - slot0 + fs;
+                const uint32_t gb = (uint32_t)(s * c.pframe) +
+                                    (c.vr ? (uint32_t)((pctr >> 8) * c.pw + (pctr & 255) + c.lp - c.vr) : 0u);
+                base[f * kMaxSnakes + k] = make_uint2(gb, (uint32_t)(k * kPatV * 8));
+            }
+        }
+        if (e + 1 < e_end) SNAKE_TBL_FETCH(e + 1);   // in flight during this env's encode
+        if (!skip) {
+            wave_sync();
+            v4u *out = reinterpret_cast<v4u *>(o.obs + (int64_t)e * c.units * 8);
+            // four chunks per lane and pass, their lookup chains interleaved
+            // (clamped reads; only the chunks that exist are stored)
+            for (int q0 = 0; q0 < chunks; q0 += 4 * kWave) {
+                v4u r[4];
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const int q = min(q0 + t * kWave + lane, chunks - 1);
+                    const uint2 dd = reinterpret_cast<const uint2 *>(desc)[q];   // units 2q, 2q + 1
+                    const uint2 b0 = base[dd.x >> 16], b1 = base[dd.y >> 16];
+                    const uint32_t v0 = pf[b0.x + (dd.x & 0xffffu)], v1 = pf[b1.x + (dd.y & 0xffffu)];
+                    const uint2 p0 = *reinterpret_cast<const uint2 *>(pat + b0.y + 8 * v0);
+                    const uint2 p1 = *reinterpret_cast<const uint2 *>(pat + b1.y + 8 * v1);
+                    r[t] = (v4u){p0.x, p0.y, p1.x, p1.y};
+                }
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    if (q0 + t * kWave + lane < chunks) obs_store(out + q0 + t * kWave + lane, r[t]);
+            }
+        }
+    }
+#undef SNAKE_TBL_FETCH
+}
+
+// NPF > 0: encode_multi<NPF>; 0: encode_one; -NPW: encode_tbl_block<NPW>
 template <int MS, int NPF, bool RO, bool JL>
 __global__ void __launch_bounds__(64) k_post(const KArgs)
 {
+    PTIME(0);
     const int G = kargs().c.reset_slots, b = (int)blockIdx.x;
     if (b < G) {
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -2096,8 +2287,10 @@ __global__ void __launch_bounds__(64) k_post(const KArgs)
     } else {
         const KArgs &A = kargs();
         if constexpr (NPF == 0) encode_one(A.c, A.st, A.o, b - G);
+        else if constexpr (NPF < 0) encode_tbl_block<-NPF>(A.c, A.st, A.o, b - G);
         else encode_multi<NPF>(A.c, A.st, A.o, b - G);
     }
+    PTIME(1);
 }
 
 // Lean encode over c.enc_per_wave consecutive envs per workgroup of T = 256
@@ -2499,6 +2692,8 @@ static void launch_post(const KCfg &k, const KArgs &a, int npf, dim3 grid, int l
 {
     const dim3 block(kWave);
     if (npf == 0) hipLaunchKernelGGL((k_post<MS, 0, RO, JL>), grid, block, lds, s, a);
+    else if (npf == -2) hipLaunchKernelGGL((k_post<MS, -2, RO, JL>), grid, block, lds, s, a);
+    else if (npf == -8) hipLaunchKernelGGL((k_post<MS, -8, RO, JL>), grid, block, lds, s, a);
     else if (npf == 1) hipLaunchKernelGGL((k_post<MS, 1, RO, JL>), grid, block, lds, s, a);
     else if (npf == 2) hipLaunchKernelGGL((k_post<MS, 2, RO, JL>), grid, block, lds, s, a);
     else hipLaunchKernelGGL((k_post<MS, 8, RO, JL>), grid, block, lds, s, a);
@@ -2630,10 +2825,12 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         // the workers, then the encodes: NPF = 16-byte ring chunks per lane the
         // two-env encode keeps in flight, 0 = one env per block
         const int epw2 = k.enc_per_wave, n16 = k.ring_bytes >> 4;
-        const int npf = epw2 <= 1 ? 0 : (n16 <= kWave ? 1 : (n16 <= 2 * kWave ? 2 : 8));
+        const int npw = (k.fs * k.HW / 4 + kWave - 1) / kWave;   // frame dwords per lane (table encode)
+        const int npf = k.tbl ? (npw <= 2 ? -2 : -8)
+                              : (epw2 <= 1 ? 0 : (n16 <= kWave ? 1 : (n16 <= 2 * kWave ? 2 : 8)));
         const int enc_blocks = npf == 0 ? k.N : (k.N + epw2 - 1) / epw2;
         const dim3 gp(k.reset_slots + enc_blocks);
-        const int lds_p = std::max(k.lds_bytes, k.lds_obs_bytes);
+        const int lds_p = std::max(k.lds_bytes, k.tbl ? k.lds_tbl_bytes : k.lds_obs_bytes);
         if (k.bg) launch_post_s<true, true>(k, a, npf, gp, lds_p, sm);   // (background boards keep the LDS record)
         else if (k.link_in_lds) launch_post_s<false, true>(k, a, npf, gp, lds_p, sm);
         else launch_post_s<false, false>(k, a, npf, gp, lds_p, sm);
@@ -2662,7 +2859,8 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
     const void *sym = !strcmp(kernel, "resets") ? (const void *)&snake::g_resets_run
                     : !strcmp(kernel, "resets_timed") ? (const void *)&snake::g_resets_timed
                     : !strcmp(kernel, "spawn_hits") ? (const void *)snake::g_spawn_hits
-                    : !strcmp(kernel, "spawn_jobs") ? (const void *)snake::g_spawn_jobs : nullptr;
+                    : !strcmp(kernel, "spawn_jobs") ? (const void *)snake::g_spawn_jobs
+                    : !strcmp(kernel, "spawn_void") ? (const void *)snake::g_spawn_void : nullptr;
     if (sym) {
         const int n = one ? 1 : snake::kDiagSlots * snake::kDiagSpread;
         std::vector<unsigned long long> v(n, 0ull), z(n, 0ull);
@@ -2730,11 +2928,14 @@ extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, in
 #endif
 
 #ifdef SNAKE_STAMPS
-// out: 64 phase stamps of block 0, then 2 * 8192 wave start/end realtimes
+// out: 64 phase stamps of block 0, 2 * 8192 k_logic wave start/end realtimes,
+// 2 * 40960 k_post block start/end realtimes
 extern "C" int snake_debug_stamps(unsigned long long *out)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_stamps), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(snake::g_wavetime),
-                               sizeof(unsigned long long) * 2 * snake::kWaveTimes) == hipSuccess ? 0 : -1;
+    if (hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(snake::g_wavetime),
+                            sizeof(unsigned long long) * 2 * snake::kWaveTimes) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out + 64 + 2 * snake::kWaveTimes, HIP_SYMBOL(snake::g_posttime),
+                               sizeof(unsigned long long) * 2 * snake::kPostTimes) == hipSuccess ? 0 : -1;
 }
 #endif

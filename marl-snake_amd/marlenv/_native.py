@@ -82,7 +82,7 @@ _libs = {}
 def lib(path=None):
     """Load libsnake_amd.so once; raise loudly when it is absent. `path` loads an
     alternative build of the same ABI (A/B timing of kernel variants)."""
-    path = path or os.environ.get('SNAKE_LIB') or LIB_PATH
+    path = path or os.environ.get("SNAKE_LIB") or LIB_PATH
     if path in _libs:
         return _libs[path]
     # PyTorch owns device memory and streams: its HIP runtime must be the one in

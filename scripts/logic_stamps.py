@@ -31,6 +31,7 @@ CFGS = {'cfg3': (65536, 4, dict(height=20, width=20, vision_range=5)),
         'cfg2': (4096, 4, dict(height=20, width=20)),
         'cfg5': (8192, 8, dict(height=40, width=40, vision_range=5, frame_stack=4))}
 KWT = 8192
+KPT = 40960
 
 
 def main():
@@ -47,7 +48,8 @@ def main():
     v.reset()
     g = torch.Generator(device='cuda').manual_seed(7)
     acts = torch.randint(0, 3, (a.skip + a.steps, N, S), generator=g, device='cuda', dtype=torch.int8)
-    buf = np.zeros(64 + 2 * KWT, np.uint64)
+    buf = np.zeros(64 + 2 * KWT + 2 * KPT, np.uint64)
+    posts = []
     nblk = (N + 64 // v.cfg.num_snakes - 1)   # upper bound; the used blocks have nonzero stamps
     rows, waves = [], []
     for t in range(a.skip + a.steps):
@@ -58,7 +60,25 @@ def main():
         L.snake_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p))
         t0 = int(buf[40])
         rows.append({n: int(buf[i]) - t0 for i, n in NAMES.items() if buf[i]})
-        wt = buf[64:].reshape(KWT, 2).astype(np.int64)
+        # k_post: worker blocks [0, reset_slots), then the encode blocks; times
+        # relative to the first k_post block's start
+        pt = buf[64 + 2 * KWT:].reshape(KPT, 2).astype(np.int64)
+        G = min(N, 2048)
+        pu = pt[:, 0] > 0
+        if pu.any():
+            p0 = pt[pu, 0].min()
+            wk, en_ = pt[:G][pu[:G]], pt[G:][pu[G:]]
+            posts.append(dict(span_ns=int((pt[pu, 1].max() - p0) * 10),
+                              workers_end_p50_ns=int((np.median(wk[:, 1]) - p0) * 10),
+                              workers_end_p90_ns=int((np.percentile(wk[:, 1], 90) - p0) * 10),
+                              workers_end_max_ns=int((wk[:, 1].max() - p0) * 10),
+                              enc_start_p50_ns=int((np.median(en_[:, 0]) - p0) * 10) if len(en_) else -1,
+                              enc_start_max_ns=int((en_[:, 0].max() - p0) * 10) if len(en_) else -1,
+                              enc_end_p50_ns=int((np.median(en_[:, 1]) - p0) * 10) if len(en_) else -1,
+                              enc_end_p99_ns=int((np.percentile(en_[:, 1], 99) - p0) * 10) if len(en_) else -1,
+                              enc_end_max_ns=int((en_[:, 1].max() - p0) * 10) if len(en_) else -1,
+                              enc_blocks_timed=int(len(en_))))
+        wt = buf[64:64 + 2 * KWT].reshape(KWT, 2).astype(np.int64)
         used = wt[:, 0] > 0
         wt = wt[used]
         s0 = wt[:, 0].min()
@@ -73,8 +93,9 @@ def main():
     med = {n: statistics.median(r[n] for r in rows if n in r) for n in NAMES.values() if any(n in r for r in rows)}
     order = sorted(med, key=med.get)
     wmed = {k: statistics.median(w[k] for w in waves) for k in waves[0]}
+    pmed = {k: statistics.median(w[k] for w in posts) for k in posts[0]} if posts else None
     print(json.dumps({'cfg': a.cfg, 'steps': len(rows), 'block0_cycles_from_start': {n: med[n] for n in order},
-                      'waves_median_over_steps': wmed}))
+                      'waves_median_over_steps': wmed, 'k_post_median_over_steps': pmed}))
 
 
 if __name__ == '__main__':
