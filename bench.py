@@ -166,6 +166,8 @@ def main():
     ap.add_argument('--num-snakes', type=int, default=None)
     ap.add_argument('--vision-range', type=int, default=None)
     ap.add_argument('--frame-stack', type=int, default=None)
+    ap.add_argument('--spawn-background', type=int, default=0,
+                    help='snake_cfg.spawn_background: 0 automatic (boards over 8 192 spawn poses), 1 on, -1 off')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--dist-backend', choices=('nccl', 'gloo'), default='nccl',
@@ -223,7 +225,8 @@ def main():
     per = args.envs_per_gpu
     n_total = per * world
     lo, hi = shard_range(n_total, world, rank)
-    venv = SnakeVecEnv(hi - lo, num_snakes=S, device=device, seed=0, env_offset=lo, **env_kw)
+    venv = SnakeVecEnv(hi - lo, num_snakes=S, device=device, seed=0, env_offset=lo,
+                       spawn_background=args.spawn_background, **env_kw)
     venv.reset()
     gen = torch.Generator(device=device)
     n_act = args.warmup + args.steps

@@ -87,9 +87,9 @@ typedef struct {
                                                          u16 draw record fits LDS (2*n_cand <= 36 KB)
                                                          and the board's auto-resets do not run beside
                                                          four-wave lean encodes (k_post_lean) */
-    int64_t spawn;      /* uint32 [N][656]               spawn-ahead record: MT key, MT pos and the
-                                                         S spawn-pose indices of the env's next reset
-                                                         ([2][N][656] with background spawn-ahead) */
+    int64_t spawn;      /* uint32 [N][672]               spawn-ahead record: MT key, MT pos and the
+                                                         S*L spawn cells (u16) of the env's next reset
+                                                         ([2][N][672] with background spawn-ahead) */
     int64_t resetq;     /* int32  2 x ([3][64][cap] + [226*32]) sharded auto-reset and spawn-ahead
                                                          queues + the step's counters, one per 128-B
                                                          line; two sets, by step parity (zero-initialised) */

@@ -16,9 +16,9 @@ constexpr int kJarrLdsMax = 36864;  // bytes of a reset's u16 draw record kept i
 constexpr int kResetSlots = 2048;   // concurrent reset workers (global link tables): 8 per CU; with k_post 2 048 beat 2 560 (cfg3 0.0905 -> 0.0892 ms; 1 536 0.106)
 constexpr int kQShards = 64;        // auto-reset queue shards (k_logic block % 64)
 constexpr int kStageMax = 8192;     // bytes of staged observation per encode group
-constexpr int kSpawnStride = 656;   // u32 words per spawn-ahead record: key, pos, poses
+constexpr int kSpawnStride = 672;   // u32 words per spawn-ahead record: key, pos, the poses' cells
 constexpr int kSpawnPos = 624;      // record word: MT position after the recorded attempts
-constexpr int kSpawnSel = 625;      // record words [625, 625 + S): spawn-pose indices
+constexpr int kSpawnCells = 625;    // record words [625, 657): the S*L spawn cells, u16, two per word
 // Queue counters (zero between steps). Every counter sits in a line of its own
 // (kQSpread words apart): same-line device-scope atomics from thousands of
 // waves serialise at the memory side.

@@ -1027,17 +1027,29 @@ __device__ __forceinline__ void mt_load_sc1(WaveMT &m, const uint32_t *g, int po
     m.pos = pos;
 }
 
-// The MT19937 state a reset of env e starts from: the spawn-ahead record when
-// one exists (the key and position after its recorded attempts), else the
-// env's own. Returns the status word (wave-uniform; the status is its bits 0-1).
-__device__ __forceinline__ int load_reset_mt(const KCfg &c, const snake_state &st, int64_t e, WaveMT &mt, int lane)
+// The MT19937 state a reset (or an in-step spawn-ahead attempt) of env e
+// starts from: the spawn-ahead record when one exists (the key and position
+// after its recorded attempts), else the env's own; cellw = this lane's word
+// of the record's spawn cells (lanes 2m, 2m + 1: word m). Returns the status
+// word (wave-uniform; the status is its bits 0-1). The state it expects (the
+// record for a reset, the env's own for an attempt, which mostly starts afresh)
+// is loaded with the status word, in the same round trip; the other one only
+// when the status asks for it. (Records are in buffer 0 without background
+// spawn-ahead.)
+__device__ __forceinline__ int load_reset_mt(const KCfg &c, const snake_state &st, int64_t e, WaveMT &mt, int lane,
+                                             bool expect_record, uint32_t &cellw)
 {
+    const uint32_t *rec = spawn_rec(c, st, e, 0);
+    const uint32_t *key = st.mt + e * kMtN;
     const int spw = st.env[e * kEnvRec + ENV_SPAWN];
-    if ((spw & 3) != SPAWN_NONE) {
-        const uint32_t *rec = spawn_rec(c, st, e, (spw >> 2) & 1);
+    if (expect_record) {
         mt_load(mt, rec, (int)rec[kSpawnPos], lane);
+        cellw = rec[kSpawnCells + (lane >> 1)];
+        if ((spw & 3) == SPAWN_NONE) mt_load(mt, key, st.env[e * kEnvRec + ENV_MTPOS], lane);
     } else {
-        mt_load(mt, st.mt + e * kMtN, st.env[e * kEnvRec + ENV_MTPOS], lane);
+        mt_load(mt, key, st.env[e * kEnvRec + ENV_MTPOS], lane);
+        cellw = 0;
+        if ((spw & 3) != SPAWN_NONE) mt_load(mt, rec, (int)rec[kSpawnPos], lane);
     }
     return spw;
 }
@@ -1046,14 +1058,16 @@ __device__ __forceinline__ int load_reset_mt(const KCfg &c, const snake_state &s
 // atomic that bumps the generation (a k_spawn job still working on the env then
 // fails its publish), and reads the record it found with sc1 loads.
 __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &st, int64_t e, WaveMT &mt,
-                                              int lane)
+                                              int lane, uint32_t &cellw)
 {
     int v = 0;
     if (lane == 0) v = (int)atomicAdd(reinterpret_cast<uint32_t *>(st.env + e * kEnvRec + ENV_SPAWN), kGenOne);
     const int spw = __shfl(v, 0);
+    cellw = 0;
     if ((spw & 3) != SPAWN_NONE) {
         const uint32_t *rec = spawn_rec(c, st, e, (spw >> 2) & 1);
         mt_load_sc1(mt, rec, (int)ld_sc1(rec + kSpawnPos), lane);
+        cellw = ld_sc1(rec + kSpawnCells + (lane >> 1));
     } else {
         mt_load(mt, st.mt + e * kMtN, st.env[e * kEnvRec + ENV_MTPOS], lane);
     }
@@ -1069,7 +1083,7 @@ __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &
 // record continues the retries where the record left them.
 template <int MS, bool JL>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
-                         WaveMT &mt, uint8_t *lds, int slot, int spw, int lane)
+                         WaveMT &mt, uint8_t *lds, int slot, int spw, uint32_t cellw, int lane)
 {
     const int spst = spw & 3;
     uint8_t *frames = lds + c.lds_frames;
@@ -1080,12 +1094,8 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
     const int sk = lane / L, si = lane - sk * L;
     int cell = -1;
     bool failed = false;
-    if (spst == SPAWN_READY) {
-        const uint32_t *rec = spawn_rec(c, st, e, (spw >> 2) & 1);
-        if (lane < SL) {
-            const uint32_t sel = c.bg ? ld_sc1(rec + kSpawnSel + sk) : rec[kSpawnSel + sk];
-            cell = (int)st.cand[(int64_t)sel * L + si];
-        }
+    if (spst == SPAWN_READY) {   // the record's cells (loaded with its key)
+        if (lane < SL) cell = (int)((cellw >> (16 * (lane & 1))) & 0xffffu);
     } else {
         // The reference retries forever; a board too crowded for S disjoint spawn
         // poses would hang the wave, so give up after 2^16 permutations and flag
@@ -1800,27 +1810,30 @@ __global__ void __launch_bounds__(64) k_logic(const KArgs)
 // a background job publishes with a compare-and-swap against it (k_spawn).
 // The record goes to buffer nb. Background (k_spawn, BG): write-through stores,
 // drained, then published with a compare-and-swap against spw.
-template <int MS, bool BG = false>
+// The spawn cells (lane < S*L: `cell`, from spawn_attempt) are stored as u16
+// pairs, lanes 2m and 2m + 1 in word m, so a reset reads them with the key.
+template <bool BG = false>
 __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, const WaveMT &mt, bool ok,
-                                   const int (&q)[MS], int lane, uint32_t spw, int nb = 0)
+                                   int cell, int lane, uint32_t spw, int nb = 0)
 {
     uint32_t *rec = spawn_rec(c, st, e, nb);
-    int mine = 0;
-#pragma unroll
-    for (int k = 0; k < MS; k++) mine = (lane == k) ? q[k] : mine;
+    // (the odd neighbour's cell: DPP quad_perm [1,0,3,2], the whole wave active)
+    const int nxt = dpp_pin(__builtin_amdgcn_mov_dpp(cell, 0xb1, 0xf, 0xf, false));
+    const uint32_t cw = ((uint32_t)cell & 0xffffu) | ((uint32_t)nxt << 16);
+    const bool cst = ok && (lane & 1) == 0 && lane < c.S * c.L;
     uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN);
     const uint32_t w1 = (spw & ~7u) | ((uint32_t)nb << 2) | (ok ? SPAWN_READY : SPAWN_PARTIAL);
     if constexpr (BG) {
 #pragma unroll
         for (int t = 0; t < 10; t++)
             if (64 * t + lane < kMtN) st_sc1(rec + 64 * t + lane, mt.w[t]);
-        if (ok && lane < c.S) st_sc1(rec + kSpawnSel + lane, (uint32_t)mine);
+        if (cst) st_sc1(rec + kSpawnCells + (lane >> 1), cw);
         if (lane == 0) st_sc1(rec + kSpawnPos, (uint32_t)mt.pos);
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) atomicCAS(wp, spw, w1);
     } else {
         mt_store(mt, rec, lane);
-        if (ok && lane < c.S) rec[kSpawnSel + lane] = (uint32_t)mine;
+        if (cst) rec[kSpawnCells + (lane >> 1)] = cw;
         if (lane == 0) {
             rec[kSpawnPos] = (uint32_t)mt.pos;
             *wp = w1;
@@ -1834,11 +1847,12 @@ template <int MS, bool JL>
 __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot, int lane)
 {
     WaveMT mt;
-    const int spw = load_reset_mt(c, st, e, mt, lane);
+    uint32_t cellw;
+    const int spw = load_reset_mt(c, st, e, mt, lane, false, cellw);
     if ((spw & 3) == SPAWN_READY) return;
     int q[MS], cell;
     const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, q, cell, lane);
-    store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)spw);
+    store_spawn_record(c, st, e, mt, ok, cell, lane, (uint32_t)spw);
 }
 
 // Background spawn-ahead job (k_spawn) of env e, queued by step t's k_logic at
@@ -1872,7 +1886,7 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
         if (a > 0) wave_sync();
         ok = spawn_attempt<MS, true>(c, st, mt, lds, 0, q, cell, lane);
     }
-    store_spawn_record<MS, true>(c, st, e, mt, ok, q, lane, spw, buf ^ 1);
+    store_spawn_record<true>(c, st, e, mt, ok, cell, lane, spw, buf ^ 1);
 }
 
 // Spawn-ahead right after an explicit reset (k_reset): the next episode's spawn
@@ -1891,7 +1905,7 @@ __device__ void spawn_after_reset(const KCfg &c, const snake_state &st, int e, W
     bool ok = false;
     for (int a = 0; a < kResetAheadTries && !ok; a++)
         ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, q, cell, lane);
-    store_spawn_record<MS>(c, st, e, mt, ok, q, lane, (uint32_t)st.env[(int64_t)e * kEnvRec + ENV_SPAWN], 0);
+    store_spawn_record(c, st, e, mt, ok, cell, lane, (uint32_t)st.env[(int64_t)e * kEnvRec + ENV_SPAWN], 0);
 }
 
 // ---------------------------------------------------- step: the observation
@@ -1974,9 +1988,11 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
             __builtin_amdgcn_s_setprio(3);
             const int e = job_env(0, idx, incl);
             WaveMT mt;
-            const int spst = J.c.bg ? claim_reset_mt(J.c, J.st, e, mt, lane) : load_reset_mt(J.c, J.st, e, mt, lane);
+            uint32_t cellw;
+            const int spst = J.c.bg ? claim_reset_mt(J.c, J.st, e, mt, lane, cellw)
+                                    : load_reset_mt(J.c, J.st, e, mt, lane, true, cellw);
             if (J.c.diag && lane == 0 && (spst & 3) == SPAWN_READY) DIAG_ADD(g_spawn_hits);
-            do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, wid, spst, lane);
+            do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, wid, spst, cellw, lane);
         } else if (!RO && idx < R + P) {
             if (J.c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
             else if (J.c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -2398,8 +2414,9 @@ __global__ void __launch_bounds__(64) k_reset(const KArgs)
         const uint8_t *mask = (const uint8_t *)J.aux;
         if (mask && !mask[e]) continue;
         WaveMT mt;
-        const int spst = load_reset_mt(J.c, J.st, e, mt, lane);
-        do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, blockIdx.x, spst, lane);
+        uint32_t cellw;
+        const int spst = load_reset_mt(J.c, J.st, e, mt, lane, true, cellw);
+        do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, blockIdx.x, spst, cellw, lane);
         // with spawn-ahead on, the next reset's poses are drawn now, off the step
         const KArgs &J2 = kargs();
         if (J2.c.spawn_thr >= 0) spawn_after_reset<MS, JL>(J2.c, J2.st, e, mt, lds, blockIdx.x, lane);

@@ -11,7 +11,7 @@ run() { local name=$1 limit=$2; shift 2; echo "== $name"; timeout -k 10 "$limit"
 if [ "${TESTS:-1}" = 1 ]; then
   run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 fi
-OUT=$OUT/lb LIBS="${LIBS:-base notbl tbl8 tbl16}" CFGS="${CFGS:-cfg3 cfg4 cfg2}" VARS=" " timeout -k 10 900 bash scripts/libbench.sh || exit 3
+OUT=$OUT/lb LIBS="${LIBS:-base prev notbl tbl8}" CFGS="${CFGS:-cfg3 cfg4 cfg2}" VARS=" " timeout -k 10 900 bash scripts/libbench.sh || exit 3
 for v in stamps stampsnotbl; do
   mkdir -p $OUT/$v && OUT=$OUT/$v LIB=marl-snake_amd/build/var/libsnake_$v.so CONFIGS="cfg3 cfg2" bash scripts/r04_stamps.sh || exit 3
 done

@@ -51,7 +51,7 @@ def test_plan_sizes(native):
     assert lay.obs == 65536 * 4 * 11 * 11 * 8
     assert lay.n_cand == 3464 and lay.jscratch == 0
     assert lay.grid_stride == 400 and lay.ring_cap == 512
-    assert lay.spawn == 65536 * 656 * 4                        # spawn-ahead records
+    assert lay.spawn == 65536 * 672 * 4                        # spawn-ahead records
     assert lay.stats == 65536 * 4 * 16                         # snake_epi_stat: one 16-B record per snake
     # two sets (step parity) of three queues + counters (one per 128-B line)
     assert lay.resetq == 2 * (3 * 64 * (4096 // 64) * 16 + 226 * 32) * 4
@@ -62,7 +62,7 @@ def test_plan_sizes(native):
     # background spawn-ahead the one-launch workers (k_post_lean) keep a global
     # link table per worker for resets without a ready record
     assert lay.n_cand == 16424 and lay.jscratch == 2048 * (16424 + 64) * 4
-    assert lay.spawn == 2 * 8192 * 656 * 4                        # background spawn-ahead: two records per env
+    assert lay.spawn == 2 * 8192 * 672 * 4                        # background spawn-ahead: two records per env
     c = cfg(native, height=44, width=44, num_snakes=4)
     lay2 = native.SnakeLayout()
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay2)) == 0
@@ -72,12 +72,12 @@ def test_plan_sizes(native):
     for kw in (dict(autoreset=False), dict(autoreset='every_step')):
         c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4, **kw)
         assert native.lib().snake_plan(ctypes.byref(c), 64, ctypes.byref(lay)) == 0
-        assert lay.jscratch == 0 and lay.spawn == 64 * 656 * 4, kw
+        assert lay.jscratch == 0 and lay.spawn == 64 * 672 * 4, kw
     # in-step spawn-ahead on that board (spawn_background=-1): one record per env,
     # the k_post_lean workers' link tables
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4, spawn_background=-1)
     assert native.lib().snake_plan(ctypes.byref(c), 64, ctypes.byref(lay)) == 0
-    assert lay.jscratch == 64 * (16424 + 64) * 4 and lay.spawn == 64 * 656 * 4
+    assert lay.jscratch == 64 * (16424 + 64) * 4 and lay.spawn == 64 * 672 * 4
 
 
 @pytest.mark.parametrize('kw,msg', [
