@@ -168,6 +168,8 @@ def main():
     ap.add_argument('--frame-stack', type=int, default=None)
     ap.add_argument('--spawn-background', type=int, default=0,
                     help='snake_cfg.spawn_background: 0 automatic (boards over 8 192 spawn poses), 1 on, -1 off')
+    ap.add_argument('--spawn-ahead', type=int, default=0,
+                    help='snake_cfg.spawn_ahead: 0 default threshold, -1 off, k: envs with at most k live snakes')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--dist-backend', choices=('nccl', 'gloo'), default='nccl',
@@ -226,7 +228,7 @@ def main():
     n_total = per * world
     lo, hi = shard_range(n_total, world, rank)
     venv = SnakeVecEnv(hi - lo, num_snakes=S, device=device, seed=0, env_offset=lo,
-                       spawn_background=args.spawn_background, **env_kw)
+                       spawn_background=args.spawn_background, spawn_ahead=args.spawn_ahead, **env_kw)
     venv.reset()
     gen = torch.Generator(device=device)
     n_act = args.warmup + args.steps
@@ -253,7 +255,7 @@ def main():
 
     L = _native.lib()
     for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_post', 'k_spawn', 'resets', 'resets_timed', 'spawn_hits',
-              'spawn_jobs', 'spawn_void'):
+              'spawn_jobs', 'spawn_void', 'reset_partial'):
         _native.timing_read(k, L)                      # drop anything from the warmup
     stride = args.timing_stride if args.timing_stride is not None else max(1, min(32, args.steps // 4))
     if distributed:
@@ -288,6 +290,7 @@ def main():
     sp_hits = _native.timing_read('spawn_hits', L)[1]
     sp_jobs = _native.timing_read('spawn_jobs', L)[1]
     sp_void = _native.timing_read('spawn_void', L)[1]
+    rs_part = _native.timing_read('reset_partial', L)[1]
     # per launch on the event-timed steps (all steps when no step is timed)
     rps_t = resets_t / n_timed if n_timed else resets / args.steps
 
@@ -355,6 +358,8 @@ def main():
                          'jobs_per_step': round(sp_jobs / n_timed, 1),
                          'jobs_per_served_reset': round(sp_jobs / max(sp_hits, 1), 3),
                          'ready_voided_per_step': round(sp_void / n_timed, 1),
+                         'resets_from_partial_per_step': round(rs_part / n_timed, 2),
+                         'resets_without_record_per_step': round((resets_t - sp_hits - rs_part) / n_timed, 2),
                          'hit_rate': round(sp_hits / max(resets_t, 1), 4)}
                         if n_timed else None),
         'cpu_baseline': None,

@@ -470,11 +470,20 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         k->logic_ms = N <= 8192 ? std::max(ms_min, 8) : ms_min;
     }
     k->q_envs_per_block = kWave / k->logic_ms;
+    {   // k_logic's LDS carve (snake_kernels.hip k_logic): E frames, the fruit buffer,
+        // the respawn raws and cells
+        const int E = k->q_envs_per_block, G = k->logic_ms;
+        k->lds_logic = E * k->grid_stride + 2 * kMaxFruits + E * G * 4 * 4 + E * G * 2;   // (kRespawnT = 4)
+    }
     k->q_cap = (int)queue_cap(N, k->q_envs_per_block);
     k->spawn_thr = spawn_thr_of(c);
     k->bg = bg ? 1 : 0;
     k->spawn_slots = (int)std::min<int64_t>(N, kResetSlots);   // k_spawn workers
     k->bg_tries = 1;   // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
+#ifndef SNAKE_SPAWN_TRIES
+#define SNAKE_SPAWN_TRIES 1
+#endif
+    k->spawn_tries = SNAKE_SPAWN_TRIES;
     k->lds_obs_bytes = off;
     {
         const LeanGeom g = lean_geom(c);
@@ -503,6 +512,8 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
 #define SNAKE_TBL_EPW 4
 #endif
     if (k->tbl) k->enc_per_wave = SNAKE_TBL_EPW;   // (the tables are built once per wave)
+    // (k_logic encoding the observations of its envs itself, from its LDS frames,
+    // measured slower: cfg3 k_logic 24.8 -> 83.9 us against k_post 66.9 -> 57.6)
     // the reset workers never use the encode staging buffer: the draw record
     // overlays it (the workers' LDS is what k_encode's waves share the CUs with)
     k->lds_link = k->lds_stage;

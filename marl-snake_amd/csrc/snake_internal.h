@@ -70,6 +70,7 @@ struct KCfg {
     uint32_t mag_n16;           // q / (grid_stride/16) == umulhi(q, mag_n16) for q < 2^32/n16
     int reset_slots;            // min(N, kResetSlots)
     int logic_ms;               // k_logic's lanes per env (its MS: 4, 8 or 16, >= S)
+    int lds_logic;              // k_logic's LDS bytes: the group's frames, the fruit buffer, respawn scratch
     int q_envs_per_block;       // envs per k_logic block (64 / logic_ms)
     int q_cap;                  // queue entries per shard
     int spawn_thr;              // queue spawn-ahead when <= this many snakes live (-1: off)
@@ -82,6 +83,7 @@ struct KCfg {
     int qpar;                   // queue set of this step (0 unless bg)
     int spawn_slots;            // k_spawn workers
     int bg_tries;               // k_spawn: permutation attempts per job (until disjoint)
+    int spawn_tries;            // in-step spawn-ahead jobs: permutation attempts per job (until disjoint)
     // lean encode (encode_lean): the frames copied into a zero-bordered LDS image
     // (lp columns / vr rows of padding, pw bytes per row, pframe bytes per frame)
     // so the crop needs no bounds test; unit -> (snake, row, col, frame) by

@@ -43,6 +43,7 @@ constexpr int kDiagSlots = 64, kDiagSpread = 16;
 __device__ unsigned long long g_spawn_hits[kDiagSlots * kDiagSpread];   // auto-resets that found a ready record
 __device__ unsigned long long g_spawn_jobs[kDiagSlots * kDiagSpread];   // spawn-ahead jobs dequeued
 __device__ unsigned long long g_spawn_void[kDiagSlots * kDiagSpread];   // ready records voided by a fruit draw
+__device__ unsigned long long g_reset_part[kDiagSlots * kDiagSpread];   // auto-resets that found a partial record
 #define DIAG_ADD(arr) atomicAdd(&(arr)[(blockIdx.x % kDiagSlots) * kDiagSpread], 1ull)
 
 #ifdef SNAKE_STAMPS
@@ -1851,7 +1852,11 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
     const int spw = load_reset_mt(c, st, e, mt, lane, false, cellw);
     if ((spw & 3) == SPAWN_READY) return;
     int q[MS], cell;
-    const bool ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, q, cell, lane);
+    bool ok = false;
+    for (int a = 0; a < c.spawn_tries && !ok; a++) {   // (attempts until disjoint, at most spawn_tries)
+        if (a > 0) wave_sync();
+        ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, q, cell, lane);
+    }
     store_spawn_record(c, st, e, mt, ok, cell, lane, (uint32_t)spw);
 }
 
@@ -1992,6 +1997,7 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
             const int spst = J.c.bg ? claim_reset_mt(J.c, J.st, e, mt, lane, cellw)
                                     : load_reset_mt(J.c, J.st, e, mt, lane, true, cellw);
             if (J.c.diag && lane == 0 && (spst & 3) == SPAWN_READY) DIAG_ADD(g_spawn_hits);
+            if (J.c.diag && lane == 0 && (spst & 3) == SPAWN_PARTIAL) DIAG_ADD(g_reset_part);
             do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, wid, spst, cellw, lane);
         } else if (!RO && idx < R + P) {
             if (J.c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
@@ -2752,7 +2758,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     DeviceGuard dg(sm);
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
     const int ms = k.logic_ms, epw = kWave / ms;   // envs per k_logic wave
-    const int lds_logic = epw * k.grid_stride + 2 * kMaxFruits + epw * ms * kRespawnT * 4 + epw * ms * 2;
+    const int lds_logic = k.lds_logic;
     const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
     // everything that can fail before k_logic fills this step's queue set
     BgCtx *bgc = nullptr;
@@ -2877,7 +2883,8 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
                     : !strcmp(kernel, "resets_timed") ? (const void *)&snake::g_resets_timed
                     : !strcmp(kernel, "spawn_hits") ? (const void *)snake::g_spawn_hits
                     : !strcmp(kernel, "spawn_jobs") ? (const void *)snake::g_spawn_jobs
-                    : !strcmp(kernel, "spawn_void") ? (const void *)snake::g_spawn_void : nullptr;
+                    : !strcmp(kernel, "spawn_void") ? (const void *)snake::g_spawn_void
+                    : !strcmp(kernel, "reset_partial") ? (const void *)snake::g_reset_part : nullptr;
     if (sym) {
         const int n = one ? 1 : snake::kDiagSlots * snake::kDiagSpread;
         std::vector<unsigned long long> v(n, 0ull), z(n, 0ull);
