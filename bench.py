@@ -209,7 +209,9 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit('--gpus N>1 needs one process per GPU: launch with torch.distributed.run')
-    distributed = world > 1
+    # under torch.distributed.run even one rank joins the process group, so the
+    # RCCL barrier / device-side max-reduce of the N-GPU line runs on a 1-GPU box
+    distributed = world > 1 or 'LOCAL_WORLD_SIZE' in os.environ
     ordinal = local_rank % max(1, torch.cuda.device_count())   # ranks beyond the GPUs share them (gloo only)
     if distributed:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
@@ -339,6 +341,7 @@ def main():
                    'height': args.height, 'width': args.width, 'num_snakes': S,
                    'vision_range': args.vision_range, 'frame_stack': args.frame_stack,
                    'snake_length': 3, 'parallelism': f'env-shard x{world}'},
+        'process_group': args.dist_backend if distributed else None,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                      'traffic': None, 'kernel': rk, 'kernel_ms': round(rk_ms, 4), 'timed_launches': n_timed,

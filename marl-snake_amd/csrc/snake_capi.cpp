@@ -246,13 +246,15 @@ static double disjoint_prob(int H, int W, int L, int S, int64_t *samples)
 // probability happens for fewer than ~2e-6 of the resets.
 constexpr double kMinDisjoint = 2e-4;
 
-// spawn-ahead threshold: by default envs with at most 2 live snakes
-// (any env under coop, where one death ends the episode); -1 = off
+// spawn-ahead threshold: by default envs with at most 3 live snakes
+// (any env under coop, where one death ends the episode); -1 = off.  Measured
+// r04h (same box, thr 2/3/4): cfg3 0.0853/0.0821/0.0900 ms, cfg4 0.0681/0.0636/
+// 0.0635, cfg2 0.0478/0.0453/0.0451, cfg5 0.1141/0.1134/0.1136.
 static int spawn_thr_of(const snake_cfg *c)
 {
     int thr;
     if (c->spawn_ahead != 0) thr = c->spawn_ahead < 0 ? -1 : c->spawn_ahead;
-    else thr = c->coop ? c->num_snakes : 2;
+    else thr = c->coop ? c->num_snakes : 3;
     if (c->autoreset != 1) thr = -1;   // (every-step resets: nothing to draw ahead)
     return thr;
 }
@@ -473,7 +475,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     {   // k_logic's LDS carve (snake_kernels.hip k_logic): E frames, the fruit buffer,
         // the respawn raws and cells
         const int E = k->q_envs_per_block, G = k->logic_ms;
-        k->lds_logic = E * k->grid_stride + 2 * kMaxFruits + E * G * 4 * 4 + E * G * 2;   // (kRespawnT = 4)
+        k->lds_logic = (int)round_up(E * k->grid_stride + 2 * kMaxFruits + E * G * 4 * 4 + E * G * 2, 16);   // (kRespawnT = 4)
     }
     k->q_cap = (int)queue_cap(N, k->q_envs_per_block);
     k->spawn_thr = spawn_thr_of(c);

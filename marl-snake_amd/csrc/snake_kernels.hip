@@ -1221,7 +1221,7 @@ __device__ __forceinline__ void logic_load(const int blk, LogicIn &in)
     const KCfg &c = A.c;
     const snake_state &st = A.st;
     constexpr int G = MS, E = kWave / MS;
-    const int lane = threadIdx.x, g = lane / G, k = lane - g * G;
+    const int lane = threadIdx.x & (kWave - 1), g = lane / G, k = lane - g * G;
     const int e0 = blk * E, e = e0 + g;
     const int S = c.S;
     const bool env_ok = e < c.N;
@@ -1252,8 +1252,9 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     const snake_out &o = A.o;
     constexpr int G = MS, E = kWave / MS;
     constexpr uint32_t gmask = (1u << G) - 1u;
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int lane = threadIdx.x, g = lane / G, k = lane - g * G, gb = g * G;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
+    uint8_t *lds = lds_all + (threadIdx.x >> 6) * c.lds_logic;   // (this wave's share of the block's LDS)
+    const int lane = threadIdx.x & (kWave - 1), g = lane / G, k = lane - g * G, gb = g * G;
     const int e0 = blk * E, e = e0 + g;
     const int S = c.S, W = c.W, cap = c.ring_cap, fs = c.fs, stride = c.grid_stride;
     const int n16 = stride >> 4;
@@ -1406,7 +1407,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     // env rejected for an invalid action: k_encode encodes its unchanged state)
     const unsigned long long qm = c.autoreset ? __ballot(env_ok && k == 0 && !bad && (ep_end || c.autoreset == 2))
                                               : 0ull;
-    const int shard = blockIdx.x % kQShards;
+    const int shard = blk % kQShards;
     int qbase = 0;
     if (qm && lane == 0) qbase = atomicAdd(&qcnt[shard * kQSpread], __popcll(qm));
 
@@ -1787,13 +1788,17 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     LSTAMP(47);
 }
 
-template <int MS>
-__global__ void __launch_bounds__(64) k_logic(const KArgs)
+// WPB waves per workgroup, each an independent group of envs (no barrier):
+// fewer, larger workgroups for the dispatcher.
+template <int MS, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_logic(const KArgs)
 {
     WTIME(0);
+    const int blk = (int)blockIdx.x * WPB + (int)(threadIdx.x >> 6);
+    if (blk * (kWave / MS) >= kargs().c.N) return;
     LogicIn in;
-    logic_load<MS>((int)blockIdx.x, in);
-    logic_body<MS>((int)blockIdx.x, in);
+    logic_load<MS>(blk, in);
+    logic_body<MS>(blk, in);
     WTIME(1);
 }
 
@@ -2773,9 +2778,14 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     }
     TimedLaunch t1("k_logic", sm);
     const KArgs la{k, st, o, actions};
-    if (ms == 4) hipLaunchKernelGGL(k_logic<4>, gl, block, lds_logic, sm, la);
-    else if (ms == 8) hipLaunchKernelGGL(k_logic<8>, gl, block, lds_logic, sm, la);
-    else hipLaunchKernelGGL(k_logic<16>, gl, block, lds_logic, sm, la);
+#ifndef SNAKE_LOGIC_WPB
+#define SNAKE_LOGIC_WPB 4   // r04i: k_logic cfg4 20.4->19.4 us, cfg5 21.9->21.1, cfg3/cfg2 neutral
+#endif
+    constexpr int WPB = SNAKE_LOGIC_WPB;
+    const dim3 glb((gl.x + WPB - 1) / WPB), blb(kWave * WPB);
+    if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB>), glb, blb, WPB * lds_logic, sm, la);
+    else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB>), glb, blb, WPB * lds_logic, sm, la);
+    else hipLaunchKernelGGL((k_logic<16, WPB>), glb, blb, WPB * lds_logic, sm, la);
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;

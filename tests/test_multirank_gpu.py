@@ -1,7 +1,9 @@
 """The N>1 bench path executed on hardware: two ranks of
 bench.main on the one GPU of the box (gloo process group: RCCL refuses two ranks
 on one device), launched as child processes through torch.distributed.run
-exactly as the driver launches N GPUs. Each rank steps its contiguous shard
+exactly as the driver launches N GPUs. A one-rank launch over RCCL (the
+driver's backend) runs the nccl process group, barrier and device-side max-reduce
+on the box's one GPU. Each rank steps its contiguous shard
 (env i seeded with its global index, actions drawn for the whole batch and
 sliced), and the concatenated shard results must equal one process stepping the
 whole batch: final grids, MT19937 keys and positions, env records, the last
@@ -63,3 +65,23 @@ def test_two_ranks_equal_one_process(tmp_path, config, per):
         assert cat.tobytes() == full[key].tobytes(), key
     if config == 'cfg3':   # the rollout went through episode ends (auto-resets on both ranks)
         assert all(int(p['env'][:, 1].min()) < 50 for p in parts)
+
+
+@pytest.mark.timeout(600)
+def test_rccl_rank_equals_plain_process(tmp_path):
+    """bench.py under torch.distributed.run with the nccl (RCCL) backend: one rank
+    on the box's GPU, the same rollout as the plain process, one JSON line whose
+    time went through the device-side all_reduce(MAX)."""
+    common = ['--steps', '30', '--warmup', '10', '--no-cpu-baseline', '--timing-stride', '4',
+              '--global-actions', '--config', 'cfg3', '--envs-per-gpu', '1024']
+    r = tmp_path / 'rccl'
+    lines = _run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+                  '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), 'bench.py', '--gpus', '1',
+                  '--dist-backend', 'nccl', '--dump-dir', str(r)] + common, tmp_path, 'rccl')
+    assert len(lines) == 1 and lines[0]['n_gpus'] == 1 and lines[0]['value'] > 0
+    assert lines[0]['process_group'] == 'nccl'
+    one = tmp_path / 'one'
+    _run([sys.executable, 'bench.py', '--dump-dir', str(one)] + common, tmp_path, 'one')
+    a, b = np.load(r / 'rank0.npz'), np.load(one / 'rank0.npz')
+    for key in ('grids', 'mt', 'mt_pos', 'env', 'obs', 'rew_sum'):
+        assert a[key].tobytes() == b[key].tobytes(), key
