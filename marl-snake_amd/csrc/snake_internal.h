@@ -13,7 +13,10 @@ constexpr int kMaxSnakes = 16;
 constexpr int kMaxFruits = 64;
 constexpr int kEnvRec = 8;          // int32 words per env record
 constexpr int kJarrLdsMax = 36864;  // bytes of a reset's u16 draw record kept in LDS
-constexpr int kResetSlots = 2048;   // concurrent reset workers (global link tables): 8 per CU; with k_post 2 048 beat 2 560 (cfg3 0.0905 -> 0.0892 ms; 1 536 0.106)
+// concurrent reset workers (global link tables): 8 per CU; with k_post 2 048 beat
+// 2 560 (round 2: cfg3 0.0905 -> 0.0892 ms; 1 536 0.106); round 4: 2 560 and 3 072
+// equal (every spawn-ahead job a first job: cfg3 0.0838 / 0.0837), 1 792 0.1016
+constexpr int kResetSlots = 2048;
 constexpr int kQShards = 64;        // auto-reset queue shards (k_logic block % 64)
 constexpr int kStageMax = 8192;     // bytes of staged observation per encode group
 constexpr int kSpawnStride = 672;   // u32 words per spawn-ahead record: key, pos, the poses' cells

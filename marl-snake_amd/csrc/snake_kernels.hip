@@ -73,8 +73,9 @@ __device__ unsigned long long g_posttime[2 * kPostTimes];   // k_post: every blo
 #define WTIME(end)                                                                 \
     do {                                                                           \
         __builtin_amdgcn_sched_barrier(0);                                         \
-        if (threadIdx.x == 0 && blockIdx.x < kWaveTimes)                           \
-            g_wavetime[2 * blockIdx.x + (end)] = __builtin_amdgcn_s_memrealtime(); \
+        const unsigned _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  \
+        if ((threadIdx.x & 63) == 0 && _w < kWaveTimes)                            \
+            g_wavetime[2 * _w + (end)] = __builtin_amdgcn_s_memrealtime();         \
         __builtin_amdgcn_sched_barrier(0);                                         \
     } while (0)
 #else
