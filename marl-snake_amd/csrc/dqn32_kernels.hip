@@ -11,8 +11,7 @@
 // matrix form needs far fewer issue slots): k_conv32_mfma for the convolutions
 // (A from an LDS patch of the input maps), k_fc32_mfma for fc1/fc2 (LDS-staged
 // tiles). k_gemm32, a 128x64-tile GEMM on the vector ALUs, runs fc3 (A <= 64
-// outputs) and the convolutions of maps too wide for the patch
-// (SNAKE_DQN32_MFMA=0 selects it for every layer). The A operand is formed on
+// outputs) and the convolutions of maps too wide for the patch. The A operand is formed on
 // the fly (no im2col buffer):
 //   kConvU8   conv1: m = (b, y, x), k = (tap, ci); X = the uint8 NHWC
 //             observation, zero outside the map (padding 1), / 255 when the
@@ -420,11 +419,9 @@ int conv_mfma(const GemmArgs &g, hipStream_t s, const char *what)
     const int64_t lds = conv_patch_bytes(g.H, g.W, g.C);
     const dim3 grid((unsigned)((g.M + kConvRows - 1) / kConvRows));
     // 4 x 2 wave tiles for the 64-channel layers (20x20x8, 16 384 observations:
-    // conv2/conv3 3 715 -> 3 666 us per launch on average, forward 9.84 -> 9.75
-    // ms; parity green); SNAKE_DQN32_WT=0 selects the 8 x 1 tiles (A/B)
-    static const char *ev_wt = getenv("SNAKE_DQN32_WT");
-    static const bool wt = !ev_wt || atoi(ev_wt) != 0;
-    if (NT == 4 && wt) hipLaunchKernelGGL((k_conv32_mfma<MODE, 4, true>), grid, dim3(256), (size_t)lds, s, g);
+    // conv2/conv3 3 715 -> 3 666 us per launch on average against 8 x 1, forward
+    // 9.84 -> 9.75 ms; parity green)
+    if constexpr (NT == 4) hipLaunchKernelGGL((k_conv32_mfma<MODE, 4, true>), grid, dim3(256), (size_t)lds, s, g);
     else hipLaunchKernelGGL((k_conv32_mfma<MODE, NT>), grid, dim3(256), (size_t)lds, s, g);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) { set_error("%s launch failed: %s", what, hipGetErrorString(err)); return SNAKE_E_LAUNCH; }
@@ -655,11 +652,8 @@ extern "C" int snake_dqn32_forward(const snake_dqn_cfg *cfg, const snake_dqn32_n
     dqn32::GemmArgs g{};
     g.H = H; g.W = W;
     // the convolutions on the matrix cores when the widest layer's LDS patch
-    // fits (every map up to ~40 wide), else the vector-ALU GEMM;
-    // SNAKE_DQN32_MFMA=0 forces the latter (A/B measurement)
-    static const char *ev = getenv("SNAKE_DQN32_MFMA");
-    const bool fc_mfma = !(ev && atoi(ev) == 0);
-    const bool mfma = fc_mfma && dqn32::conv_patch_bytes(H, W, std::max(C, 64)) <= dqn32::kPatchMaxBytes;
+    // fits (every map up to ~40 wide), else the vector-ALU GEMM
+    const bool mfma = dqn32::conv_patch_bytes(H, W, std::max(C, 64)) <= dqn32::kPatchMaxBytes;
     // conv1: uint8 NHWC obs -> Y1 [B*P][32]
     g.x = obs; g.xbias = nullptr; g.w = net->conv1_w; g.y = sc.y1; g.ybias = nullptr;
     g.M = BP; g.N = 32; g.K = 9 * C; g.C = C; g.scale_flag = sc.flag;
@@ -678,11 +672,11 @@ extern "C" int snake_dqn32_forward(const snake_dqn_cfg *cfg, const snake_dqn32_n
     // fc1: relu(Y3 + b3) flattened NHWC (P*64) -> Y4 [B][256]
     g.x = sc.y3; g.xbias = net->conv3_b; g.bmod = 64; g.w = net->fc1_w; g.y = sc.y4;
     g.M = batch; g.N = 256; g.K = (int)(P * 64);
-    if ((rc = fc_mfma ? dqn32::fc_mfma(g, s, "fc1") : dqn32::gemm<dqn32::kDense>(g, s, "fc1"))) return rc;
+    if ((rc = dqn32::fc_mfma(g, s, "fc1"))) return rc;
     // fc2: relu(Y4 + bfc1) -> Y5 [B][128]
     g.x = sc.y4; g.xbias = net->fc1_b; g.bmod = 256; g.w = net->fc2_w; g.y = sc.y5;
     g.N = 128; g.K = 256;
-    if ((rc = fc_mfma ? dqn32::fc_mfma(g, s, "fc2") : dqn32::gemm<dqn32::kDense>(g, s, "fc2"))) return rc;
+    if ((rc = dqn32::fc_mfma(g, s, "fc2"))) return rc;
     // fc3: relu(Y5 + bfc2) -> q [B][A] + bfc3
     g.x = sc.y5; g.xbias = net->fc2_b; g.bmod = 128; g.w = net->fc3_w; g.y = q_out; g.ybias = net->fc3_b;
     g.N = A; g.K = 128;

@@ -597,19 +597,10 @@ const ConvTable<1> kConv1;
 const ConvTable<2> kConv2;
 const ConvTable<4> kConv4;
 int g_conv_grid[3][5][3];
-// waves per observation in k_dqn_conv when snake_dqn_cfg.conv_waves is 0:
-// SNAKE_DQN_WAVES=1|2|4, else 4 (two for odd row-tile counts). Forward at 262144
-// observations: 4.51 / 4.57 / 5.91 ms for 4 / 2 / 1.
-int conv_waves()
-{
-    static int nw = 0;
-    if (!nw) {
-        const char *e = getenv("SNAKE_DQN_WAVES");
-        const int v = e ? atoi(e) : 0;
-        nw = (v == 1 || v == 2) ? v : 4;
-    }
-    return nw;
-}
+// waves per observation in k_dqn_conv when snake_dqn_cfg.conv_waves is 0: 4
+// (two for odd row-tile counts). Forward at 262144 observations: 4.51 / 4.57 /
+// 5.91 ms for 4 / 2 / 1 (conv_waves selects the others).
+int conv_waves() { return 4; }
 }  // namespace
 
 extern "C" int snake_dqn_plan(const snake_dqn_cfg *cfg, snake_dqn_layout *out)

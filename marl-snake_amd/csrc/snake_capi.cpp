@@ -482,10 +482,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->bg = bg ? 1 : 0;
     k->spawn_slots = (int)std::min<int64_t>(N, kResetSlots);   // k_spawn workers
     k->bg_tries = 1;   // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
-#ifndef SNAKE_SPAWN_TRIES
-#define SNAKE_SPAWN_TRIES 1
-#endif
-    k->spawn_tries = SNAKE_SPAWN_TRIES;
+    k->spawn_tries = 1;   // attempts per in-step spawn-ahead job (2 measured cfg3 0.0875 -> 0.103 ms: a retry doubles the chain)
     k->lds_obs_bytes = off;
     {
         const LeanGeom g = lean_geom(c);
@@ -494,26 +491,20 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         k->mag_ups = g.mag_ups; k->mag_rowl = g.mag_rowl; k->mag_fs = g.mag_fs; k->mag_wpr = g.mag_wpr;
         // the table encode (snake_kernels.hip encode_tbl_block) where k_post runs
         // the encodes: rings of at most 512 dwords, the lean geometry exact
-#ifndef SNAKE_ENC_TBL
-#define SNAKE_ENC_TBL 1
-#endif
         const int64_t fdw = (int64_t)k->fs * k->HW / 4;
         int t = 0;
         k->tbl_base = (int)round_up((int64_t)k->fs * k->pframe, 16); t = k->tbl_base + 8 * k->fs * kMaxSnakes;
         k->tbl_pat = t; t += 8 * k->S * 160;   // (kPatV)
         k->tbl_desc = t; t += (int)round_up(4 * (int64_t)k->units, 16);
         k->lds_tbl_bytes = t;
-        k->tbl = SNAKE_ENC_TBL && g.exact && !g.lean && fdw <= 8 * kWave && t <= 40 * 1024 ? 1 : 0;
+        k->tbl = g.exact && !g.lean && fdw <= 8 * kWave && t <= 40 * 1024 ? 1 : 0;
     }
     // envs per encode wave (k_post's encodes: the next env's ring prefetched into
     // registers, at most 8 16-byte chunks per lane): two at 16 384 envs and more
     // (cfg3 0.1033 -> 0.0998 ms; 4, 8, 16, 32 measured 0.1016, 0.106, 0.114,
     // 0.135), one below (cfg2 0.0622 vs 0.0625); the lean encode two per workgroup
     k->enc_per_wave = k->lean ? 2 : (N >= 16384 && k->ring_bytes <= 8 * 1024 ? 2 : 1);
-#ifndef SNAKE_TBL_EPW
-#define SNAKE_TBL_EPW 4
-#endif
-    if (k->tbl) k->enc_per_wave = SNAKE_TBL_EPW;   // (the tables are built once per wave)
+    if (k->tbl) k->enc_per_wave = 4;   // (the tables are built once per wave; 8 measured slower at cfg3)
     // (k_logic encoding the observations of its envs itself, from its LDS frames,
     // measured slower: cfg3 k_logic 24.8 -> 83.9 us against k_post 66.9 -> 57.6)
     // the reset workers never use the encode staging buffer: the draw record

@@ -192,9 +192,6 @@ template <int G, int J>
 __device__ __forceinline__ int gsel(int v)
 {
     static_assert(G == 4 || G == 8 || G == 16, "group of 4, 8 or 16 lanes");
-#ifdef SNAKE_NO_DPP
-    return __shfl(v, (int)(threadIdx.x & ~(G - 1)) + J);
-#endif
     if constexpr (G == 4) {
         return dpp_pin(__builtin_amdgcn_mov_dpp(v, J * 0x55, 0xf, 0xf, false));   // quad_perm:[J,J,J,J]
     } else if constexpr (G == 16) {
@@ -221,13 +218,6 @@ __device__ __forceinline__ double gsel(double v)
 template <int G>
 __device__ __forceinline__ int gscan(int v, int k)
 {
-#ifdef SNAKE_NO_DPP
-    for (int o = 1; o < G; o <<= 1) {
-        const int n = __shfl_up(v, o);
-        if (k >= o) v += n;
-    }
-    return v;
-#endif
     int x = dpp_pin(__builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));   // row_shr:1
     v += k >= 1 ? x : 0;
     x = dpp_pin(__builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));       // row_shr:2
@@ -2779,10 +2769,9 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     }
     TimedLaunch t1("k_logic", sm);
     const KArgs la{k, st, o, actions};
-#ifndef SNAKE_LOGIC_WPB
-#define SNAKE_LOGIC_WPB 4   // r04i: k_logic cfg4 20.4->19.4 us, cfg5 21.9->21.1, cfg3/cfg2 neutral
-#endif
-    constexpr int WPB = SNAKE_LOGIC_WPB;
+    // four waves (groups) per workgroup: k_logic cfg4 20.4 -> 19.4 us, cfg5 21.9
+    // -> 21.1 against one, cfg3 and cfg2 unchanged (round 4)
+    constexpr int WPB = 4;
     const dim3 glb((gl.x + WPB - 1) / WPB), blb(kWave * WPB);
     if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB>), glb, blb, WPB * lds_logic, sm, la);
     else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB>), glb, blb, WPB * lds_logic, sm, la);
