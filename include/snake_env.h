@@ -90,7 +90,7 @@ typedef struct {
     int64_t spawn;      /* uint32 [N][672]               spawn-ahead record: MT key, MT pos and the
                                                          S*L spawn cells (u16) of the env's next reset
                                                          ([2][N][672] with background spawn-ahead) */
-    int64_t resetq;     /* int32  2 x ([3][64][cap] + [226*32]) sharded auto-reset and spawn-ahead
+    int64_t resetq;     /* int32  2 x ([3][64][cap] + [227*32]) sharded auto-reset and spawn-ahead
                                                          queues + the step's counters, one per 128-B
                                                          line; two sets, by step parity (zero-initialised) */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */

@@ -32,7 +32,12 @@ constexpr int kQClaim = kNumQ * kQShards;             // counter index of claim 
 constexpr int kQDone = kQClaim + kClaimShards;        // counter index: claim shards drained
 constexpr int kQSpClaim = kQDone + 1;                 // background spawn kernel (k_spawn): claim shard 0
 constexpr int kQSpDone = kQSpClaim + kClaimShards;    // k_spawn: claim shards drained
-constexpr int kQCount = kQSpDone + 1;                 // counters
+// k_spawn launches on this set that have finished (each one's last worker adds
+// one after re-zeroing the set's spawn counters; never zeroed): k_logic queues
+// spawn-ahead jobs into the set only when it equals KCfg.spawn_gate, the count
+// launched so far, instead of the step waiting for the background stream
+constexpr int kQSpGen = kQSpDone + 1;
+constexpr int kQCount = kQSpGen + 1;                  // counters
 constexpr int kQCounters = kQCount * kQSpread;        // words
 // The queues and counters exist twice (the step's parity, KCfg.qpar): with the
 // background spawn kernel a step's spawn-ahead queues are still being read while
@@ -87,6 +92,7 @@ struct KCfg {
     int spawn_slots;            // k_spawn workers
     int bg_tries;               // k_spawn: permutation attempts per job (until disjoint)
     int spawn_tries;            // in-step spawn-ahead jobs: permutation attempts per job (until disjoint)
+    uint32_t spawn_gate;        // bg: k_spawn launches on this step's queue set so far (kQSpGen)
     // lean encode (encode_lean): the frames copied into a zero-bordered LDS image
     // (lp columns / vr rows of padding, pw bytes per row, pframe bytes per frame)
     // so the crop needs no bounds test; unit -> (snake, row, col, frame) by

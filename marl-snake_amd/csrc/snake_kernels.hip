@@ -1203,6 +1203,7 @@ struct LogicIn {
     int4 er, er2, rec;
     uint4 sv;
     int act;
+    uint32_t gate;   // bg: the queue set's finished spawn-kernel count (lane 0)
 };
 
 template <int MS>
@@ -1219,6 +1220,11 @@ __device__ __forceinline__ void logic_load(const int blk, LogicIn &in)
     in.er = in.er2 = in.rec = make_int4(0, 0, 0, 0);
     in.sv = make_uint4(0, 0, 0, 0);
     in.act = 0;
+    in.gate = 0;
+    if (c.bg && lane == 0) {
+        const int *qc = st.resetq + (int64_t)c.qpar * (kNumQ * kQShards * c.q_cap + kQCounters) + kNumQ * kQShards * c.q_cap;
+        in.gate = ld_sc1(reinterpret_cast<const uint32_t *>(&qc[kQSpGen * kQSpread]));
+    }
     if (env_ok) {
         in.er = *reinterpret_cast<const int4 *>(st.env + (int64_t)e * kEnvRec);
         // loaded whatever the threshold: a step run with spawn-ahead off must
@@ -1429,8 +1435,10 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     // by its job); the status word written below is the exact one.
     // urgent (at most one live snake: the reset is likely next) and other jobs
     const bool urgent = __popc(am) <= 1;
-    const bool spawn_q = c.spawn_thr >= 0 && env_ok && !bad && !ep_end && (need ? true : spst != SPAWN_READY) &&
-                         __popc(am) <= c.spawn_thr;
+    // (background: only into a queue set its spawn kernels have finished with)
+    const bool set_free = !c.bg || (uint32_t)bcast((int)in.gate, 0) == c.spawn_gate;
+    const bool spawn_q = c.spawn_thr >= 0 && set_free && env_ok && !bad && !ep_end &&
+                         (need ? true : spst != SPAWN_READY) && __popc(am) <= c.spawn_thr;
     const unsigned long long pm = __ballot(spawn_q && urgent && k == 0);
     const unsigned long long pn = __ballot(spawn_q && !urgent && k == 0);
     int pbase = 0, nbase = 0;
@@ -2023,7 +2031,7 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
         int d = 0;
         if (lane == 0) d = atomicAdd(&qc[kQDone * kQSpread], 1);
         if (bcast(d, 0) == nsh - 1)   // (background: the reset counters only)
-            for (int q = lane; q < kQCount; q += kWave)
+            for (int q = lane; q < kQSpGen; q += kWave)
                 if (!c.bg || q < kQShards || (q >= kQClaim && q <= kQDone)) qc[q * kQSpread] = 0;
     }
 }
@@ -2091,8 +2099,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kResetW
         int d = 0;
         if (lane == 0) d = atomicAdd(&qc[kQSpDone * kQSpread], 1);
         if (bcast(d, 0) == nsh - 1) {
-            for (int q = kQShards + lane; q < kNumQ * kQShards; q += kWave) qc[q * kQSpread] = 0;
-            if (lane <= kClaimShards) qc[(kQSpClaim + lane) * kQSpread] = 0;   // (claims + done)
+            // write-through zeroes, drained, then the set's finished count: a
+            // k_logic that reads the count (sc1) then adds to these counters
+            // from any XCD (MI355X_MICROARCH.md, inter-workgroup hand-off)
+            for (int q = kQShards + lane; q < kNumQ * kQShards; q += kWave)
+                st_sc1(reinterpret_cast<uint32_t *>(&qc[q * kQSpread]), 0u);
+            if (lane <= kClaimShards) st_sc1(reinterpret_cast<uint32_t *>(&qc[(kQSpClaim + lane) * kQSpread]), 0u);   // (claims + done)
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) atomicAdd(reinterpret_cast<unsigned *>(&qc[kQSpGen * kQSpread]), 1u);
         }
     }
 }
@@ -2593,6 +2607,7 @@ struct BgCtx {
     hipEvent_t done[2] = {nullptr, nullptr};
     uint64_t steps = 0;
     bool pending[2] = {false, false};
+    uint32_t launched[2] = {0, 0};   // k_spawn launches per queue set (KCfg.spawn_gate)
 };
 static std::mutex g_bgmu;
 static std::map<const void *, BgCtx> g_bg;
@@ -2758,14 +2773,13 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     const dim3 g1(k.N), gl((k.N + epw - 1) / epw), gr(k.reset_slots), block(kWave);
     // everything that can fail before k_logic fills this step's queue set
     BgCtx *bgc = nullptr;
-    if (k.bg) {   // background spawn-ahead: this step's queue set, once the
-                  // spawn kernel of two steps ago has read it
+    if (k.bg) {   // background spawn-ahead: this step's queue set; k_logic queues
+                  // spawn-ahead jobs into it only if the spawn kernels launched on
+                  // it so far have finished (kQSpGen), the stream never waits
+                  // (the wait cost cfg5 0.1026 -> 0.1136 ms per step)
         if (!(bgc = bg_ctx(st, true))) return SNAKE_E_LAUNCH;
         k.qpar = (int)(bgc->steps & 1);
-        if (bgc->pending[k.qpar] && hipStreamWaitEvent(sm, bgc->done[k.qpar], 0) != hipSuccess) {
-            set_error("ordering after the background spawn kernel failed");
-            return SNAKE_E_LAUNCH;
-        }
+        k.spawn_gate = bgc->launched[k.qpar];
     }
     TimedLaunch t1("k_logic", sm);
     const KArgs la{k, st, o, actions};
@@ -2784,7 +2798,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     auto fail = [&](int r) {
         int *qc = st.resetq + (int64_t)k.qpar * (kNumQ * kQShards * k.q_cap + kQCounters) +
                   kNumQ * kQShards * k.q_cap;
-        (void)hipMemsetAsync(qc, 0, sizeof(int) * kQCounters, sm);
+        (void)hipMemsetAsync(qc, 0, sizeof(int) * kQSpGen * kQSpread, sm);   // (not the finished count)
         return r;
     };
     const KArgs a{k, st, o, nullptr};
@@ -2828,6 +2842,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
             return fail(SNAKE_E_LAUNCH);
         }
         bgc->pending[k.qpar] = true;
+        bgc->launched[k.qpar]++;
         bgc->steps++;
     }
     TimedLaunch t2("k_post", sm);

@@ -61,8 +61,13 @@ def test_two_ranks_equal_one_process(tmp_path, config, per):
     parts = [np.load(two / f'rank{r}.npz') for r in range(2)]
     assert [(int(p['lo']), int(p['hi'])) for p in parts] == [(0, per), (per, 2 * per)]
     for key in ('grids', 'mt', 'mt_pos', 'env', 'obs', 'rew_sum'):
-        cat = np.concatenate([p[key] for p in parts])
-        assert cat.tobytes() == full[key].tobytes(), key
+        cat, ref = np.concatenate([p[key] for p in parts]), full[key]
+        if key == 'env' and config == 'cfg5':
+            # background spawn-ahead (40x40): the status word (ENV_SPAWN, word 4:
+            # record status + generation) depends on when each k_spawn finished
+            # relative to the steps -- bookkeeping, not env state
+            cat, ref = np.delete(cat, 4, axis=1), np.delete(ref, 4, axis=1)
+        assert cat.tobytes() == ref.tobytes(), key
     if config == 'cfg3':   # the rollout went through episode ends (auto-resets on both ranks)
         assert all(int(p['env'][:, 1].min()) < 50 for p in parts)
 
