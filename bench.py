@@ -20,21 +20,23 @@ A step = one SnakeVecEnv.step() over the GPU's whole batch. The timed region is
 exactly K steps between barrier + synchronize on both sides; value = all envs of
 all ranks x K / the slowest rank's time.
 
-A step is two launches at cfg2/cfg3 (include/snake_env.h snake_step): k_logic
-(rules, all envs), then k_post, whose first blocks are the reset workers (the
-step's auto-resets, then the spawn-ahead attempts: next resets' permutations
-drawn early) and the rest the observations of every other env. Where k_post
-does not apply (background spawn-ahead, cfg5) the workers (k_autoreset) and the
-encodes (k_encode) are two launches forked onto two streams.
+A step is two launches on the caller's stream (include/snake_env.h snake_step):
+k_logic (rules, all envs), then k_post, whose first blocks are the reset workers
+(the step's auto-resets, then the spawn-ahead attempts: next resets'
+permutations drawn early) and the rest the observations of every other env. On
+boards of more than 8 192 spawn poses (cfg5) it is k_post_lean (resets-only
+workers + four-wave lean encodes) and the spawn-ahead attempts run in k_spawn on
+a background stream the step never waits for.
 
 The JSON line also carries:
   roofline     -- the kernel that moves the bulk of SURVEY.md 8(d)'s bytes:
-                  k_post (or k_encode), per launch (N - resets) x (S*h*w*8*fs obs
+                  k_post (k_post_lean at cfg5), per launch (N - resets) x (S*h*w*8*fs obs
                   write + fs*H*W frame reads) [+ for k_post, per reset 2 MT keys +
                   fs*H*W + S*h*w*8*fs, per spawn-ahead attempt 2 MT keys + the
                   pose indices] / its average duration, timed by the library's HIP
                   timing events on its own stream during the timed region
-                  (snake_timing_enable; every --timing-stride-th step, default 32),
+                  (snake_timing_enable; every --timing-stride-th step, default
+                  max(1, min(32, steps // 4)) so that >= 4 launches are averaged),
                   against the 8 TB/s HBM peak; `traffic` is null (the HBM bytes of
                   a launch come from rocprofv3 PMC passes, committed under
                   profiles/, which a plain run cannot read).

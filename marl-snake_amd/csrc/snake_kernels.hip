@@ -1206,7 +1206,7 @@ struct LogicIn {
     uint32_t gate;   // bg: the queue set's finished spawn-kernel count (lane 0)
 };
 
-template <int MS>
+template <int MS, bool BG>
 __device__ __forceinline__ void logic_load(const int blk, LogicIn &in)
 {
     const KArgs &A = kargs();
@@ -1221,7 +1221,7 @@ __device__ __forceinline__ void logic_load(const int blk, LogicIn &in)
     in.sv = make_uint4(0, 0, 0, 0);
     in.act = 0;
     in.gate = 0;
-    if (c.bg && lane == 0) {
+    if (BG && lane == 0) {
         const int *qc = st.resetq + (int64_t)c.qpar * (kNumQ * kQShards * c.q_cap + kQCounters) + kNumQ * kQShards * c.q_cap;
         in.gate = ld_sc1(reinterpret_cast<const uint32_t *>(&qc[kQSpGen * kQSpread]));
     }
@@ -1239,7 +1239,7 @@ __device__ __forceinline__ void logic_load(const int blk, LogicIn &in)
     }
 }
 
-template <int MS>
+template <int MS, bool BG>
 __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
 {
     LSTAMP(40);
@@ -1436,7 +1436,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     // urgent (at most one live snake: the reset is likely next) and other jobs
     const bool urgent = __popc(am) <= 1;
     // (background: only into a queue set its spawn kernels have finished with)
-    const bool set_free = !c.bg || (uint32_t)bcast((int)in.gate, 0) == c.spawn_gate;
+    const bool set_free = !BG || (uint32_t)bcast((int)in.gate, 0) == c.spawn_gate;
     const bool spawn_q = c.spawn_thr >= 0 && set_free && env_ok && !bad && !ep_end &&
                          (need ? true : spst != SPAWN_READY) && __popc(am) <= c.spawn_thr;
     const unsigned long long pm = __ballot(spawn_q && urgent && k == 0);
@@ -1696,7 +1696,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     // (a draw bumps the record's generation: a background attempt started from the
     // old state (k_spawn) then fails its final compare-and-swap, or, if that landed
     // first, is overwritten here; so with bg every draw writes the word)
-    const bool spw_wr = drew && (c.bg || spst != SPAWN_NONE);
+    const bool spw_wr = drew && (BG || spst != SPAWN_NONE);
     if (c.diag && drew && spst == SPAWN_READY && k == 0) DIAG_ADD(g_spawn_void);
     const uint32_t spw1 = drew ? (((uint32_t)er2.x >> 3) + 1u) << 3 : (uint32_t)er2.x;
 
@@ -1723,7 +1723,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
         if ((qm >> lane) & 1ull) qb[shard * c.q_cap + base + mbcnt64(qm)] = e;
     }
     // and the spawn-ahead jobs (background: with the generation they were queued at)
-    const int pent = c.bg ? (int)((uint32_t)e | ((spw1 >> 3) << (32 - kQGenBits))) : e;
+    const int pent = BG ? (int)((uint32_t)e | ((spw1 >> 3) << (32 - kQGenBits))) : e;
     if (pm) {
         const int base = bcast(pbase, 0);
         if ((pm >> lane) & 1ull) qb[(kQShards + shard) * c.q_cap + base + mbcnt64(pm)] = pent;
@@ -1733,7 +1733,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
         if ((pn >> lane) & 1ull) qb[(2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn)] = pent;
     }
     if (env_ok && k == 0 && !bad && spw_wr) {
-        if (c.bg) atomicExch(reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN), spw1);
+        if (BG) atomicExch(reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN), spw1);
         else st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)spw1;
     }
     LSTAMP(49);
@@ -1789,15 +1789,17 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
 
 // WPB waves per workgroup, each an independent group of envs (no barrier):
 // fewer, larger workgroups for the dispatcher.
-template <int MS, int WPB>
+// BG: background spawn-ahead (KCfg.bg), its queue-set gate and status-word
+// atomics; the in-step form carries none of it
+template <int MS, int WPB, bool BG>
 __global__ void __launch_bounds__(64 * WPB) k_logic(const KArgs)
 {
     WTIME(0);
     const int blk = (int)blockIdx.x * WPB + (int)(threadIdx.x >> 6);
     if (blk * (kWave / MS) >= kargs().c.N) return;
     LogicIn in;
-    logic_load<MS>(blk, in);
-    logic_body<MS>(blk, in);
+    logic_load<MS, BG>(blk, in);
+    logic_body<MS, BG>(blk, in);
     WTIME(1);
 }
 
@@ -2787,9 +2789,15 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     // -> 21.1 against one, cfg3 and cfg2 unchanged (round 4)
     constexpr int WPB = 4;
     const dim3 glb((gl.x + WPB - 1) / WPB), blb(kWave * WPB);
-    if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB>), glb, blb, WPB * lds_logic, sm, la);
-    else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB>), glb, blb, WPB * lds_logic, sm, la);
-    else hipLaunchKernelGGL((k_logic<16, WPB>), glb, blb, WPB * lds_logic, sm, la);
+    if (k.bg) {
+        if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+        else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+        else hipLaunchKernelGGL((k_logic<16, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+    } else {
+        if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+        else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+        else hipLaunchKernelGGL((k_logic<16, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+    }
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;
