@@ -448,8 +448,18 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     }
     k->link_stride = (int)round_up(k->n_cand, 4) + kWave;
     // the LDS draw record: u16 per index < n_cand + one dummy slot per lane
-    const int jbytes = (int)round_up(2 * ((int64_t)k->n_cand + kWave), 16);
+    int jbytes = (int)round_up(2 * ((int64_t)k->n_cand + kWave), 16);
     k->link_in_lds = jbytes <= kJarrLdsMax;
+    // up to 32 768 envs the attempts' chain sets the shared phase: their link
+    // table as u32 in LDS (ds_min while drawing, then a pointer chase of ~ln n
+    // hops instead of scanning the u16 record: ~15 K of ~60 K cycles per
+    // attempt) -- cfg2 0.0451 -> 0.0430 ms, cfg4 0.0627 -> 0.0602; at 65 536
+    // envs the doubled LDS costs the encodes their occupancy (cfg3 0.0842 ->
+    // 0.0994), so there the u16 record stays
+    if (k->link_in_lds && N <= 32768 && !bg_of(c, n_cand) && 4 * (int64_t)k->link_stride <= kJarrLdsMax) {
+        k->link32 = 1;
+        jbytes = 4 * k->link_stride;
+    }
     // reset workers (<= kResetSlots, the global link tables are sized for that)
     k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
     const bool bg = bg_of(c, n_cand);

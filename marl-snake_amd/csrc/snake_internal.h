@@ -68,6 +68,7 @@ struct KCfg {
     // worker's u32 link table in global scratch, link_stride = round4(n_cand) + 64
     // per-lane dummies entries per table
     int link_stride;
+    int link32;                 // the LDS link table as u32 (ds_min) + pointer chase instead of the u16 record + scan (JL = 2)
     int lds_obs_bytes;          // LDS of k_encode: no reset worker state
     // row-wise encode through an LDS staging buffer (encode_rows): snakes per
     // staged group (0: direct encode), the buffer, and magic reciprocals of

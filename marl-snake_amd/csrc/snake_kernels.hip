@@ -950,18 +950,32 @@ __device__ __forceinline__ int dir_of_diff(int diff, int W)
 // permutation(n_cand)[:S] drawn from the wave's MT, lane (sk, si) = cell si of
 // pose sk (-1 past S*L), q = the pose indices; true when the poses are disjoint
 // (_clear_overlap :568-574).
-template <int MS, bool JL>
+template <int MS, int JL>
 __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, uint8_t *lds, int slot,
                               int (&q)[MS], int &cell, int lane)
 {
     const int S = c.S, L = c.L, SL = S * L;
     const int sk = lane / L, si = lane - sk * L;
-    if constexpr (JL) {
-        // the u16 draw record in LDS: every index 1..n-1 is written, nothing to clear
-        lu16 *jarr = (lu16 *)(lds + c.lds_link);
-        mt_perm_draws(mt, c.n_cand, S, jarr, c.n_cand, jarr, lane);
-        wave_sync();
-        perm_trace_j<MS>(S, c.n_cand, jarr, q, lane);
+    if constexpr (JL == 2) {
+        {
+            // small batches: the u32 link table in LDS (ds_min, no scan: the
+            // trace is a short pointer chase)
+            lu32 *link = (lu32 *)(lds + c.lds_link);
+            lu16 *jsmall = (lu16 *)(lds + c.lds_fruit);   // the fruit buffer is free until place_fruits
+            for (int x = 4 * lane; x < c.link_stride - kWave; x += 4 * kWave) *(lu4 *)(link + x) = (v4u32)kNoLink;
+            wave_sync();
+            mt_perm_draws(mt, c.n_cand, S, link, c.n_cand, jsmall, lane);
+            wave_sync();
+            perm_trace<MS>(S, link, jsmall, q, lane);
+        }
+    } else if constexpr (JL == 1) {
+        {
+            // the u16 draw record in LDS: every index 1..n-1 is written, nothing to clear
+            lu16 *jarr = (lu16 *)(lds + c.lds_link);
+            mt_perm_draws(mt, c.n_cand, S, jarr, c.n_cand, jarr, lane);
+            wave_sync();
+            perm_trace_j<MS>(S, c.n_cand, jarr, q, lane);
+        }
     } else {
         // large boards: the link table in this worker's global scratch
         gu32 *link = (gu32 *)(st.jscratch + (int64_t)slot * c.link_stride);
@@ -1073,7 +1087,7 @@ __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &
 // over the frame stack. `mt` comes from load_reset_mt: with a ready spawn-ahead
 // record the poses are the record's and the draws are already done; a partial
 // record continues the retries where the record left them.
-template <int MS, bool JL>
+template <int MS, int JL>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
                          WaveMT &mt, uint8_t *lds, int slot, int spw, uint32_t cellw, int lane)
 {
@@ -1850,7 +1864,7 @@ __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, 
 
 // The in-step spawn-ahead job of env e: one attempt from its MT state or its
 // partial record, into record buffer 0.
-template <int MS, bool JL>
+template <int MS, int JL>
 __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *lds, int slot, int lane)
 {
     WaveMT mt;
@@ -1895,7 +1909,7 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
     bool ok = false;
     for (int a = 0; a < c.bg_tries && !ok; a++) {   // (attempts until disjoint, at most bg_tries)
         if (a > 0) wave_sync();
-        ok = spawn_attempt<MS, true>(c, st, mt, lds, 0, q, cell, lane);
+        ok = spawn_attempt<MS, 1>(c, st, mt, lds, 0, q, cell, lane);
     }
     store_spawn_record<true>(c, st, e, mt, ok, cell, lane, spw, buf ^ 1);
 }
@@ -1907,7 +1921,7 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
 // exactly what the next reset would draw (spawn-ahead semantics, snake_step).
 constexpr int kResetAheadTries = 4;
 
-template <int MS, bool JL>
+template <int MS, int JL>
 __device__ void spawn_after_reset(const KCfg &c, const snake_state &st, int e, WaveMT &mt, uint8_t *lds,
                                   int slot, int lane)
 {
@@ -1945,10 +1959,11 @@ __device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st,
 }
 
 // RO: resets only (every-step mode, background spawn-ahead): no spawn-job path,
-// fewer registers. JL: the draw record in LDS (KCfg.link_in_lds), else the
+// fewer registers. JL: 1 the u16 draw record in LDS (KCfg.link_in_lds), 2 the
+// u32 link table in LDS (KCfg.link32, batches of up to 32 768 envs), 0 the
 // global link tables; one path per instantiation.
 // wid = this worker (0 .. G-1): k_autoreset's block, or a block of k_post.
-template <int MS, bool RO, bool JL>
+template <int MS, bool RO, int JL>
 __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uint8_t *lds)
 {
     const int lane = threadIdx.x & (kWave - 1);
@@ -2038,7 +2053,7 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
     }
 }
 
-template <int MS, bool RO, bool JL>
+template <int MS, bool RO, int JL>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kResetWavesPerEU))) k_autoreset(const KArgs)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -2194,8 +2209,9 @@ __device__ __forceinline__ void encode_multi(const KCfg &c, const snake_state &s
 // encode_one; else encode_multi<NPF>). Dispatched in block order, so the workers
 // go first; one launch instead of a fork onto a side stream and a join (round 3:
 // cfg3 0.0970 -> 0.0941 ms, cfg2 0.0591 -> 0.0539); the kernel's registers and
-// LDS are the larger of the two. JL: the workers' draw record in LDS, else their
-// global link tables (boards of more than 18 368 spawn poses).
+// LDS are the larger of the two. JL: the workers' draw record (1) or u32 link
+// table (2) in LDS, else their global link tables (boards of more than 18 368
+// spawn poses).
 // ---------------------------------------------------------- table encode
 // The observation of c.enc_per_wave consecutive envs per wave (_encode
 // snake_env.py:474-519 + the frame stack :444-472) as table lookups. Per 8-byte
@@ -2310,7 +2326,7 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
 }
 
 // NPF > 0: encode_multi<NPF>; 0: encode_one; -NPW: encode_tbl_block<NPW>
-template <int MS, int NPF, bool RO, bool JL>
+template <int MS, int NPF, bool RO, int JL>
 __global__ void __launch_bounds__(64) k_post(const KArgs)
 {
     PTIME(0);
@@ -2413,14 +2429,14 @@ __global__ void __launch_bounds__(256) k_post_lean(const KArgs)
     const int G = kargs().c.reset_slots, GB = (G + 3) >> 2, b = (int)blockIdx.x;
     if (b < GB) {
         const int wave = (int)(threadIdx.x >> 6), wid = 4 * b + wave;
-        if (wid < G) autoreset_worker<MS, RO, false>(wid, G, lds + wave * kargs().c.lds_worker);
+        if (wid < G) autoreset_worker<MS, RO, 0>(wid, G, lds + wave * kargs().c.lds_worker);
     } else {
         const KArgs &A = kargs();
         encode_lean_block<8, 256>(A.c, A.st, A.o, b - GB);
     }
 }
 
-template <int MS, bool JL>
+template <int MS, int JL>
 __global__ void __launch_bounds__(64) k_reset(const KArgs)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -2709,21 +2725,25 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
     TimedLaunch tl("k_reset", (hipStream_t)stream);
     const KArgs a{k, st, o, mask};
     const hipStream_t s = (hipStream_t)stream;
-    if (k.link_in_lds) {
-        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, true>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, true>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_reset<16, true>), grid, block, k.lds_bytes, s, a);
+    if (k.link32) {
+        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, 2>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, 2>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_reset<16, 2>), grid, block, k.lds_bytes, s, a);
+    } else if (k.link_in_lds) {
+        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, 1>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, 1>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_reset<16, 1>), grid, block, k.lds_bytes, s, a);
     } else {
-        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, false>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, false>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_reset<16, false>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, 0>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, 0>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_reset<16, 0>), grid, block, k.lds_bytes, s, a);
     }
     tl.close();
     return check_launch("k_reset");
 }
 
 // k_post<MS(S), NPF, RO, JL> (see k_post)
-template <int MS, bool RO, bool JL>
+template <int MS, bool RO, int JL>
 static void launch_post(const KCfg &k, const KArgs &a, int npf, dim3 grid, int lds, hipStream_t s)
 {
     const dim3 block(kWave);
@@ -2735,7 +2755,7 @@ static void launch_post(const KCfg &k, const KArgs &a, int npf, dim3 grid, int l
     else hipLaunchKernelGGL((k_post<MS, 8, RO, JL>), grid, block, lds, s, a);
 }
 
-template <bool RO, bool JL>
+template <bool RO, int JL>
 static void launch_post_s(const KCfg &k, const KArgs &a, int npf, dim3 grid, int lds, hipStream_t s)
 {
     if (k.S <= 4) launch_post<4, RO, JL>(k, a, npf, grid, lds, s);
@@ -2748,13 +2768,13 @@ static void launch_autoreset_ro(const KCfg &k, const KArgs &a, dim3 grid, hipStr
 {
     const dim3 block(kWave);
     if (k.link_in_lds) {
-        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true, true>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true, true>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_autoreset<16, true, true>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true, 1>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true, 1>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_autoreset<16, true, 1>), grid, block, k.lds_bytes, s, a);
     } else {
-        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true, false>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true, false>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_autoreset<16, true, false>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true, 0>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true, 0>), grid, block, k.lds_bytes, s, a);
+        else hipLaunchKernelGGL((k_autoreset<16, true, 0>), grid, block, k.lds_bytes, s, a);
     }
 }
 
@@ -2877,9 +2897,10 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         const int enc_blocks = npf == 0 ? k.N : (k.N + epw2 - 1) / epw2;
         const dim3 gp(k.reset_slots + enc_blocks);
         const int lds_p = std::max(k.lds_bytes, k.tbl ? k.lds_tbl_bytes : k.lds_obs_bytes);
-        if (k.bg) launch_post_s<true, true>(k, a, npf, gp, lds_p, sm);   // (background boards keep the LDS record)
-        else if (k.link_in_lds) launch_post_s<false, true>(k, a, npf, gp, lds_p, sm);
-        else launch_post_s<false, false>(k, a, npf, gp, lds_p, sm);
+        if (k.bg) launch_post_s<true, 1>(k, a, npf, gp, lds_p, sm);   // (background boards keep the LDS record)
+        else if (k.link32) launch_post_s<false, 2>(k, a, npf, gp, lds_p, sm);
+        else if (k.link_in_lds) launch_post_s<false, 1>(k, a, npf, gp, lds_p, sm);
+        else launch_post_s<false, 0>(k, a, npf, gp, lds_p, sm);
     }
     t2.close();
     if ((rc = check_launch("k_post"))) return fail(rc);
