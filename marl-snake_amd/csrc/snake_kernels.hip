@@ -2335,6 +2335,9 @@ __global__ void __launch_bounds__(64) k_post(const KArgs)
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
         autoreset_worker<MS, RO, JL>(b, G, lds);
     } else {
+#ifdef SNAKE_DIAG_NO_ENCODE   // (diagnostic build: instruction counts without the encodes)
+        return;
+#endif
         const KArgs &A = kargs();
         if constexpr (NPF == 0) encode_one(A.c, A.st, A.o, b - G);
         else if constexpr (NPF < 0) encode_tbl_block<-NPF>(A.c, A.st, A.o, b - G);
