@@ -2283,6 +2283,15 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
     } while (0)
     if (e_begin < e_end) SNAKE_TBL_FETCH(e_begin);
     const int chunks = c.units >> 1;
+    // a lane's chunks all in one pass (cfg3: 242 chunks): their descriptors in
+    // registers for every env of the wave, one LDS level less per lookup chain
+    const bool one = chunks <= 4 * kWave;
+    uint2 dr[4];
+    if (one) {
+        wave_sync();
+#pragma unroll
+        for (int t = 0; t < 4; t++) dr[t] = reinterpret_cast<const uint2 *>(desc)[min(t * kWave + lane, chunks - 1)];
+    }
     for (int e = e_begin; e < e_end; e++) {
         const int cur = pcur, skip = pskip;   // (a reset env's obs is written by its reset)
         wave_sync();                          // (the previous encode has read the LDS image)
@@ -2302,20 +2311,28 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
         if (!skip) {
             wave_sync();
             v4u *out = reinterpret_cast<v4u *>(o.obs + (int64_t)e * c.units * 8);
+            auto lookup = [&](uint2 dd) {   // units 2q, 2q + 1 of descriptor pair dd
+                const uint2 b0 = base[dd.x >> 16], b1 = base[dd.y >> 16];
+                const uint32_t v0 = pf[b0.x + (dd.x & 0xffffu)], v1 = pf[b1.x + (dd.y & 0xffffu)];
+                const uint2 p0 = *reinterpret_cast<const uint2 *>(pat + b0.y + 8 * v0);
+                const uint2 p1 = *reinterpret_cast<const uint2 *>(pat + b1.y + 8 * v1);
+                return (v4u){p0.x, p0.y, p1.x, p1.y};
+            };
+            if (one) {
+                v4u r[4];
+#pragma unroll
+                for (int t = 0; t < 4; t++) r[t] = lookup(dr[t]);
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    if (t * kWave + lane < chunks) obs_store(out + t * kWave + lane, r[t]);
+            } else
             // four chunks per lane and pass, their lookup chains interleaved
             // (clamped reads; only the chunks that exist are stored)
             for (int q0 = 0; q0 < chunks; q0 += 4 * kWave) {
                 v4u r[4];
 #pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const int q = min(q0 + t * kWave + lane, chunks - 1);
-                    const uint2 dd = reinterpret_cast<const uint2 *>(desc)[q];   // units 2q, 2q + 1
-                    const uint2 b0 = base[dd.x >> 16], b1 = base[dd.y >> 16];
-                    const uint32_t v0 = pf[b0.x + (dd.x & 0xffffu)], v1 = pf[b1.x + (dd.y & 0xffffu)];
-                    const uint2 p0 = *reinterpret_cast<const uint2 *>(pat + b0.y + 8 * v0);
-                    const uint2 p1 = *reinterpret_cast<const uint2 *>(pat + b1.y + 8 * v1);
-                    r[t] = (v4u){p0.x, p0.y, p1.x, p1.y};
-                }
+                for (int t = 0; t < 4; t++)
+                    r[t] = lookup(reinterpret_cast<const uint2 *>(desc)[min(q0 + t * kWave + lane, chunks - 1)]);
 #pragma unroll
                 for (int t = 0; t < 4; t++)
                     if (q0 + t * kWave + lane < chunks) obs_store(out + q0 + t * kWave + lane, r[t]);
