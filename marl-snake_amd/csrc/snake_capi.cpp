@@ -508,13 +508,17 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         k->tbl_desc = t; t += (int)round_up(4 * (int64_t)k->units, 16);
         k->lds_tbl_bytes = t;
         k->tbl = g.exact && !g.lean && fdw <= 8 * kWave && t <= 40 * 1024 ? 1 : 0;
+        // also in k_post_lean's four-wave workgroups (tables shared by the
+        // workgroup, two envs each): cfg5 0.1023-0.1031 -> 0.1013-0.1015 ms; four
+        // or eight envs per workgroup 0.107 / 0.111
+        if (g.lean && t <= 48 * 1024) k->tbl = 1;
     }
     // envs per encode wave (k_post's encodes: the next env's ring prefetched into
     // registers, at most 8 16-byte chunks per lane): two at 16 384 envs and more
     // (cfg3 0.1033 -> 0.0998 ms; 4, 8, 16, 32 measured 0.1016, 0.106, 0.114,
     // 0.135), one below (cfg2 0.0622 vs 0.0625); the lean encode two per workgroup
     k->enc_per_wave = k->lean ? 2 : (N >= 16384 && k->ring_bytes <= 8 * 1024 ? 2 : 1);
-    if (k->tbl) k->enc_per_wave = 4;   // (the tables are built once per wave; 8 measured slower at cfg3)
+    if (k->tbl) k->enc_per_wave = k->lean ? 2 : 4;   // (the tables are built once per wave; 8 measured slower at cfg3)
     // (k_logic encoding the observations of its envs itself, from its LDS frames,
     // measured slower: cfg3 k_logic 24.8 -> 83.9 us against k_post 66.9 -> 57.6)
     // the reset workers never use the encode staging buffer: the draw record

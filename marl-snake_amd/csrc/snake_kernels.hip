@@ -2228,7 +2228,14 @@ __device__ __forceinline__ void encode_multi(const KCfg &c, const snake_state &s
 // are loaded into registers during this env's encode (as encode_lean_block).
 constexpr int kPatV = 160;   // grid byte values 10 * id + code (id < 16, code <= 5)
 
-template <int NPW>
+template <int T>
+__device__ __forceinline__ void tsync()
+{
+    if constexpr (T == kWave) wave_sync();
+    else __syncthreads();
+}
+
+template <int NPW, int T = kWave>
 __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const snake_out &o, const int blk)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -2247,7 +2254,7 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
     int src[NPW], dst[NPW];
 #pragma unroll
     for (int u = 0; u < NPW; u++) {
-        const int x = min(lane + u * kWave, nwt - 1);
+        const int x = min(lane + u * T, nwt - 1);
         const int s = x / nw, xx = x - s * nw;
         const int r = fdiv((uint32_t)xx, c.mag_wpr, wpr), c4 = xx - r * wpr;
         src[u] = s * gsw + xx;
@@ -2255,15 +2262,15 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
     }
     // once per wave: the zero image, the patterns of the codes that occur (0, 1,
     // 2 and 10 * id + 3..5 for id < S), the unit descriptors
-    zero_lean<kWave>(c, pf, lane);
+    zero_lean<T>(c, pf, lane);
     const int npv = 3 + 3 * S;   // occurring codes per snake
-    for (int x = lane; x < S * npv; x += kWave) {
+    for (int x = lane; x < S * npv; x += T) {
         const int k = x / npv, r = x - k * npv;
         const int v = r < 3 ? r : 10 * ((r - 3) / 3) + 3 + (r - 3) % 3;
         const unsigned long long b = onehot(v, k);
         reinterpret_cast<uint2 *>(pat)[k * kPatV + v] = make_uint2((uint32_t)b, (uint32_t)(b >> 32));
     }
-    for (int u = lane; u < c.units; u += kWave) {
+    for (int u = lane; u < c.units; u += T) {
         const int kk = (int)__umulhi((uint32_t)u, c.mag_ups), r0 = u - kk * c.ups;
         const int ii = (int)__umulhi((uint32_t)r0, c.mag_rowl), r1 = r0 - ii * c.rowl;
         const int jj = fdiv((uint32_t)r1, c.mag_fs, fs), ff = r1 - jj * fs;
@@ -2285,16 +2292,16 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
     const int chunks = c.units >> 1;
     // a lane's chunks all in one pass (cfg3: 242 chunks): their descriptors in
     // registers for every env of the wave, one LDS level less per lookup chain
-    const bool one = chunks <= 4 * kWave;
+    const bool one = T == kWave && chunks <= 4 * T;
     uint2 dr[4];
-    if (one) {
-        wave_sync();
+    if constexpr (T == kWave) if (one) {
+        tsync<T>();
 #pragma unroll
-        for (int t = 0; t < 4; t++) dr[t] = reinterpret_cast<const uint2 *>(desc)[min(t * kWave + lane, chunks - 1)];
+        for (int t = 0; t < 4; t++) dr[t] = reinterpret_cast<const uint2 *>(desc)[min(t * T + lane, chunks - 1)];
     }
     for (int e = e_begin; e < e_end; e++) {
         const int cur = pcur, skip = pskip;   // (a reset env's obs is written by its reset)
-        wave_sync();                          // (the previous encode has read the LDS image)
+        tsync<T>();                          // (the previous encode has read the LDS image)
         if (!skip) {
 #pragma unroll
             for (int u = 0; u < NPW; u++) reinterpret_cast<uint32_t *>(pf)[dst[u]] = w[u];
@@ -2309,7 +2316,7 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
         }
         if (e + 1 < e_end) SNAKE_TBL_FETCH(e + 1);   // in flight during this env's encode
         if (!skip) {
-            wave_sync();
+            tsync<T>();
             v4u *out = reinterpret_cast<v4u *>(o.obs + (int64_t)e * c.units * 8);
             auto lookup = [&](uint2 dd) {   // units 2q, 2q + 1 of descriptor pair dd
                 const uint2 b0 = base[dd.x >> 16], b1 = base[dd.y >> 16];
@@ -2318,24 +2325,27 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
                 const uint2 p1 = *reinterpret_cast<const uint2 *>(pat + b1.y + 8 * v1);
                 return (v4u){p0.x, p0.y, p1.x, p1.y};
             };
-            if (one) {
+            if (T == kWave && one) {
                 v4u r[4];
 #pragma unroll
                 for (int t = 0; t < 4; t++) r[t] = lookup(dr[t]);
 #pragma unroll
                 for (int t = 0; t < 4; t++)
-                    if (t * kWave + lane < chunks) obs_store(out + t * kWave + lane, r[t]);
-            } else
-            // four chunks per lane and pass, their lookup chains interleaved
-            // (clamped reads; only the chunks that exist are stored)
-            for (int q0 = 0; q0 < chunks; q0 += 4 * kWave) {
-                v4u r[4];
+                    if (t * T + lane < chunks) obs_store(out + t * T + lane, r[t]);
+            } else {
+            // CP chunks per lane and pass, their lookup chains interleaved
+            // (clamped reads; only the chunks that exist are stored); two in
+            // four-wave workgroups (register budget)
+            constexpr int CP = T == kWave ? 4 : 2;
+            for (int q0 = 0; q0 < chunks; q0 += CP * T) {
+                v4u r[CP];
 #pragma unroll
-                for (int t = 0; t < 4; t++)
-                    r[t] = lookup(reinterpret_cast<const uint2 *>(desc)[min(q0 + t * kWave + lane, chunks - 1)]);
+                for (int t = 0; t < CP; t++)
+                    r[t] = lookup(reinterpret_cast<const uint2 *>(desc)[min(q0 + t * T + lane, chunks - 1)]);
 #pragma unroll
-                for (int t = 0; t < 4; t++)
-                    if (q0 + t * kWave + lane < chunks) obs_store(out + q0 + t * kWave + lane, r[t]);
+                for (int t = 0; t < CP; t++)
+                    if (q0 + t * T + lane < chunks) obs_store(out + q0 + t * T + lane, r[t]);
+            }
             }
         }
     }
@@ -2442,7 +2452,7 @@ __device__ __forceinline__ void encode_lean_block(const KCfg &c, const snake_sta
 // these boards), the workers run the resets only; else also the in-step
 // spawn-ahead attempts. One launch instead of the fork/join of round 2 (12 and
 // 16 us of cross-stream latency per step at cfg5).
-template <int MS, bool RO>
+template <int MS, bool RO, bool TBL>
 __global__ void __launch_bounds__(256) k_post_lean(const KArgs)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -2452,7 +2462,8 @@ __global__ void __launch_bounds__(256) k_post_lean(const KArgs)
         if (wid < G) autoreset_worker<MS, RO, 0>(wid, G, lds + wave * kargs().c.lds_worker);
     } else {
         const KArgs &A = kargs();
-        encode_lean_block<8, 256>(A.c, A.st, A.o, b - GB);
+        if constexpr (TBL) encode_tbl_block<8, 256>(A.c, A.st, A.o, b - GB);
+        else encode_lean_block<8, 256>(A.c, A.st, A.o, b - GB);
     }
 }
 
@@ -2897,15 +2908,25 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     if (k.lean) {
         // four workers per workgroup, then the four-wave lean encodes
         const dim3 gp((k.reset_slots + 3) / 4 + (k.N + k.enc_per_wave - 1) / k.enc_per_wave);
-        const int lds_p = std::max(4 * k.lds_worker, k.lds_lean_bytes);
-        if (k.bg) {
-            if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, true>), gp, dim3(256), lds_p, sm, a);
-            else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, true>), gp, dim3(256), lds_p, sm, a);
-            else hipLaunchKernelGGL((k_post_lean<16, true>), gp, dim3(256), lds_p, sm, a);
+        const int lds_p = std::max(4 * k.lds_worker, k.tbl ? k.lds_tbl_bytes : k.lds_lean_bytes);
+        if (k.tbl) {   // (the table encode in four-wave workgroups)
+            if (k.bg) {
+                if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, true, true>), gp, dim3(256), lds_p, sm, a);
+                else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, true, true>), gp, dim3(256), lds_p, sm, a);
+                else hipLaunchKernelGGL((k_post_lean<16, true, true>), gp, dim3(256), lds_p, sm, a);
+            } else {
+                if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, false, true>), gp, dim3(256), lds_p, sm, a);
+                else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, false, true>), gp, dim3(256), lds_p, sm, a);
+                else hipLaunchKernelGGL((k_post_lean<16, false, true>), gp, dim3(256), lds_p, sm, a);
+            }
+        } else if (k.bg) {
+            if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, true, false>), gp, dim3(256), lds_p, sm, a);
+            else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, true, false>), gp, dim3(256), lds_p, sm, a);
+            else hipLaunchKernelGGL((k_post_lean<16, true, false>), gp, dim3(256), lds_p, sm, a);
         } else {
-            if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, false>), gp, dim3(256), lds_p, sm, a);
-            else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, false>), gp, dim3(256), lds_p, sm, a);
-            else hipLaunchKernelGGL((k_post_lean<16, false>), gp, dim3(256), lds_p, sm, a);
+            if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, false, false>), gp, dim3(256), lds_p, sm, a);
+            else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, false, false>), gp, dim3(256), lds_p, sm, a);
+            else hipLaunchKernelGGL((k_post_lean<16, false, false>), gp, dim3(256), lds_p, sm, a);
         }
     } else {
         // the workers, then the encodes: NPF = 16-byte ring chunks per lane the
