@@ -466,7 +466,7 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // spawn-ahead jobs at 1, below the encodes; small batches with in-step
     // spawn-ahead at 3 (a lone attempt is there the step's critical path: cfg2
     // 0.0510 -> 0.0494 ms; at cfg3 it costs 0.0905 -> 0.0960)
-    k->spawn_prio = N <= 8192 && !bg ? 3 : 1;
+    k->spawn_prio = N <= 32768 && !bg ? 3 : 1;   // (round 4, with the LDS link table: cfg4 0.0595 -> 0.0584 ms)
     // the encodes above the spawn-ahead jobs: the bandwidth-bound encodes then
     // keep HBM busy while the compute-bound workers fill the issue gaps (cfg3
     // 0.1275 -> 0.1200 ms against the hardware default 0). With background

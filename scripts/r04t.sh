@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4: cost of the main stream's wait on the background spawn kernel
-# (diagnostic SNAKE_BG_NOWAIT build: the wait dropped, timing only).
+# (diagnostic SNAKE_BG_NOWAIT build of that time: the wait dropped, timing only;
+# the product has since dropped the wait for a device-side gate).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${OUT:-gpurun_out/r04t}
