@@ -481,12 +481,24 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         const int ms_min = k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16);
         k->logic_ms = N <= 8192 ? std::max(ms_min, 8) : ms_min;
     }
-    k->q_envs_per_block = kWave / k->logic_ms;
-    {   // k_logic's LDS carve (snake_kernels.hip k_logic): E frames, the fruit buffer,
-        // the respawn raws and cells
-        const int E = k->q_envs_per_block, G = k->logic_ms;
-        k->lds_logic = (int)round_up(E * k->grid_stride + 2 * kMaxFruits + E * G * 4 * 4 + E * G * 2, 16);   // (kRespawnT = 4)
+    // k_logic's LDS carve (snake_kernels.hip k_logic) per wave: E frames, the
+    // fruit buffer, the respawn raws and cells
+    auto logic_lds = [&](int G) {
+        const int E = kWave / G;
+        return (int)round_up((int64_t)E * k->grid_stride + 2 * kMaxFruits + E * G * 4 * 4 + E * G * 2, 16);   // (kRespawnT = 4)
+    };
+    // large boards: fewer envs per wave until one wave's frames fit a workgroup
+    while (k->logic_ms < 16 && logic_lds(k->logic_ms) > kLdsLimit) k->logic_ms *= 2;
+    k->lds_logic = logic_lds(k->logic_ms);
+    if (k->lds_logic > kLdsLimit) {
+        set_error("%dx%d board: k_logic's %d frames per wave (%d bytes) do not fit the %d-byte LDS", k->H, k->W,
+                  kWave / k->logic_ms, k->lds_logic, kLdsLimit);
+        return SNAKE_E_CONFIG;
     }
+    // four independent waves per workgroup where their LDS fits (round 4: k_logic
+    // cfg4 20.4 -> 19.4 us, cfg5 21.9 -> 21.1 against one), else one
+    k->logic_wpb = 4 * (int64_t)k->lds_logic <= kLdsLimit ? 4 : 1;
+    k->q_envs_per_block = kWave / k->logic_ms;
     k->q_cap = (int)queue_cap(N, k->q_envs_per_block);
     k->spawn_thr = spawn_thr_of(c);
     k->bg = bg ? 1 : 0;
@@ -615,7 +627,11 @@ int snake_plan(const snake_cfg *cfg, int64_t num_envs, snake_layout *out)
 {
     if (!out) { set_error("out is NULL"); return SNAKE_E_ARG; }
     g_err[0] = 0;
-    return layout_of(cfg, num_envs, out);
+    int rc = layout_of(cfg, num_envs, out);
+    if (rc) return rc;
+    // (and every launch-side limit: a config the step cannot launch fails here)
+    KCfg k;
+    return build_kcfg(cfg, num_envs, out->n_cand, &k);
 }
 
 int64_t snake_build_candidates(const snake_cfg *cfg, int16_t *host_out, int64_t capacity)

@@ -13,6 +13,7 @@ constexpr int kMaxSnakes = 16;
 constexpr int kMaxFruits = 64;
 constexpr int kEnvRec = 8;          // int32 words per env record
 constexpr int kJarrLdsMax = 36864;  // bytes of a reset's u16 draw record kept in LDS
+constexpr int kLdsLimit = 160 * 1024;   // LDS per workgroup (gfx950)
 // concurrent reset workers (global link tables): 8 per CU; with k_post 2 048 beat
 // 2 560 (round 2: cfg3 0.0905 -> 0.0892 ms; 1 536 0.106); round 4: 2 560 and 3 072
 // equal (every spawn-ahead job a first job: cfg3 0.0838 / 0.0837), 1 792 0.1016
@@ -79,7 +80,8 @@ struct KCfg {
     uint32_t mag_n16;           // q / (grid_stride/16) == umulhi(q, mag_n16) for q < 2^32/n16
     int reset_slots;            // min(N, kResetSlots)
     int logic_ms;               // k_logic's lanes per env (its MS: 4, 8 or 16, >= S)
-    int lds_logic;              // k_logic's LDS bytes: the group's frames, the fruit buffer, respawn scratch
+    int lds_logic;              // k_logic's LDS bytes per wave: the group's frames, the fruit buffer, respawn scratch
+    int logic_wpb;              // k_logic's waves per workgroup (4, or 1 where 4 * lds_logic exceeds kLdsLimit)
     int q_envs_per_block;       // envs per k_logic block (64 / logic_ms)
     int q_cap;                  // queue entries per shard
     int spawn_thr;              // queue spawn-ahead when <= this many snakes live (-1: off)

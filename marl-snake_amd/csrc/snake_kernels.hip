@@ -2836,19 +2836,23 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     }
     TimedLaunch t1("k_logic", sm);
     const KArgs la{k, st, o, actions};
-    // four waves (groups) per workgroup: k_logic cfg4 20.4 -> 19.4 us, cfg5 21.9
-    // -> 21.1 against one, cfg3 and cfg2 unchanged (round 4)
-    constexpr int WPB = 4;
-    const dim3 glb((gl.x + WPB - 1) / WPB), blb(kWave * WPB);
-    if (k.bg) {
-        if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
-        else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
-        else hipLaunchKernelGGL((k_logic<16, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
-    } else {
-        if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
-        else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
-        else hipLaunchKernelGGL((k_logic<16, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
-    }
+    // four waves (groups) per workgroup where their LDS fits (KCfg.logic_wpb):
+    // k_logic cfg4 20.4 -> 19.4 us, cfg5 21.9 -> 21.1 against one (round 4)
+    auto launch_logic = [&](auto wpb) {
+        constexpr int WPB = decltype(wpb)::value;
+        const dim3 glb((gl.x + WPB - 1) / WPB), blb(kWave * WPB);
+        if (k.bg) {
+            if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+            else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+            else hipLaunchKernelGGL((k_logic<16, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+        } else {
+            if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+            else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+            else hipLaunchKernelGGL((k_logic<16, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+        }
+    };
+    if (k.logic_wpb == 4) launch_logic(std::integral_constant<int, 4>{});
+    else launch_logic(std::integral_constant<int, 1>{});
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;

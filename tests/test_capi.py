@@ -80,6 +80,18 @@ def test_plan_sizes(native):
     assert lay.jscratch == 64 * (16424 + 64) * 4 and lay.spawn == 64 * 672 * 4
 
 
+@pytest.mark.parametrize('H,W,L,N', [(50, 50, 3, 16384), (72, 72, 3, 4096), (100, 100, 2, 65536)])
+def test_plan_large_boards(native, H, W, L, N):
+    """Boards whose k_logic frames do not fit four waves per workgroup (ADVICE r4:
+    4 x 41 KB at 50x50 and 16 envs per wave) still plan: snake_plan runs the
+    launch-side checks too (build_kcfg), which pick one wave per workgroup or
+    fewer envs per wave instead of a launch that fails."""
+    c = cfg(native, height=H, width=W, snake_length=L, num_snakes=4, vision_range=3)
+    lay = native.SnakeLayout()
+    assert native.lib().snake_plan(ctypes.byref(c), N, ctypes.byref(lay)) == 0, \
+        native.lib().snake_last_error().decode()
+
+
 @pytest.mark.parametrize('kw,msg', [
     (dict(num_snakes=0), 'num_snakes'), (dict(num_snakes=17), 'num_snakes'),
     (dict(snake_length=1), 'snake_length'), (dict(height=2), 'height'),

@@ -145,6 +145,8 @@ BATCH_CASES = {
     'spawn_all_40_s8': (dict(height=40, width=40, snake_length=3, vision_range=5, spawn_ahead=8), 8, 16, 250),
     # 20 168 spawn poses: the reset workers' global link tables (no LDS draw record)
     'big_44_s4_global_links': (dict(height=44, width=44, snake_length=3, vision_range=4, spawn_ahead=4), 4, 16, 200),
+    # 100x100: k_logic's eight frames per wave take 80 KB of LDS, one wave per workgroup
+    'big_100_l2': (dict(height=100, width=100, snake_length=2, vision_range=3), 4, 16, 120),
 }
 
 
@@ -207,14 +209,27 @@ def test_shards_equal_full_batch():
         assert torch.equal(df, torch.cat([x[2] for x in outs]))
 
 
-def test_full_size_sampled_parity(oracle):
-    """BASELINE config 3 at full size (65 536 envs): a sample of envs replayed
-    through the oracle bit-exactly, plus whole-batch invariants. 400 steps reach
-    the steady regime the bench times (past 200 steps almost every reset starts
-    from a spawn-ahead record)."""
+FULL_SIZE_CASES = {
+    # BASELINE config 3: the u16 draw record, 4-lane k_logic
+    'cfg3_65536': (65536, 4, 400, dict(height=20, width=20, snake_length=3, vision_range=5)),
+    # config 4's per-GPU shard (262 144 / 8): the u32 LDS link table, 4-lane
+    # k_logic, 16 envs per k_logic wave -- the instantiation the 8-GPU headline runs
+    'cfg4_32768': (32768, 4, 400, dict(height=20, width=20, snake_length=3, vision_range=5)),
+    # 50x50 (26 000+ spawn poses): global link tables, in-step spawn-ahead, and
+    # k_logic with one wave per workgroup (four would need 162 KB of LDS)
+    'big50_16384': (16384, 4, 200, dict(height=50, width=50, snake_length=3, vision_range=4)),
+}
+
+
+@pytest.mark.parametrize('case', sorted(FULL_SIZE_CASES))
+def test_full_size_sampled_parity(oracle, case):
+    """Full-size batches: a sample of envs replayed through the oracle
+    bit-exactly, plus whole-batch invariants. 400 steps reach the steady regime
+    the bench times (past 200 steps almost every reset starts from a spawn-ahead
+    record)."""
     from marlenv import SnakeVecEnv
-    N, S, T = 65536, 4, 400
-    kw = dict(height=20, width=20, snake_length=3, vision_range=5)
+    N, S, T, kw = FULL_SIZE_CASES[case]
+    vr = kw['vision_range']
     v = SnakeVecEnv(N, num_snakes=S, seed=0, **kw)
     obs = v.reset()
     idx = np.unique(np.concatenate([np.arange(8), np.linspace(0, N - 1, 40).astype(int),
@@ -233,14 +248,14 @@ def test_full_size_sampled_parity(oracle):
         sub = {k: x[sel].cpu().numpy() for k, x in info.items()}
         compare_step([refs[int(i)] for i in idx], range(len(idx)), a[sel].cpu().numpy(),
                      obs[sel].cpu().numpy(), rew[sel].cpu().numpy(), done[sel].cpu().numpy(), sub,
-                     where=f'full-size step {t}')
+                     where=f'{case} step {t}')
         # invariants over every env (every 10th step): one own-head cell at the
         # crop centre of each alive snake; no own-head channel for dead snakes
         if t % 10:
             continue
         tab = v.snake_table()
         alive = tab[..., 5].bool()
-        centre = obs[:, :, 5, 5, 5]
+        centre = obs[:, :, vr, vr, 5]
         heads = obs[..., 5].sum(dim=(2, 3))
         assert torch.equal(centre.bool() | ~alive, torch.ones_like(alive))
         assert torch.equal(heads[alive], torch.ones_like(heads[alive]))
