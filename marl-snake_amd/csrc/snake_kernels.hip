@@ -78,7 +78,29 @@ __device__ unsigned long long g_posttime[2 * kPostTimes];   // k_post: every blo
             g_wavetime[2 * _w + (end)] = __builtin_amdgcn_s_memrealtime();         \
         __builtin_amdgcn_sched_barrier(0);                                         \
     } while (0)
+// every reset-worker item (scripts/post_items.py): worker | type << 32, start,
+// end (s_memrealtime), env; types 0 reset from a ready record, 1 from a partial
+// one, 2 without one, 3 queue-1 spawn-ahead job, 4 queue-2 job
+constexpr int kItems = 16384;
+__device__ unsigned g_nitems;
+__device__ unsigned long long g_items[4 * kItems];
+#define ITEM_T0() const unsigned long long _it0 = __builtin_amdgcn_s_memrealtime()
+#define ITEM_LOG(wid, type, e)                                                                      \
+    do {                                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+        const unsigned long long _it1 = __builtin_amdgcn_s_memrealtime();                          \
+        if ((threadIdx.x & 63) == 0) {                                                             \
+            const unsigned _i = atomicAdd(&g_nitems, 1u);                                          \
+            if (_i < kItems) {                                                                     \
+                g_items[4 * _i] = (unsigned long long)(wid) | ((unsigned long long)(type) << 32);   \
+                g_items[4 * _i + 1] = _it0; g_items[4 * _i + 2] = _it1;                             \
+                g_items[4 * _i + 3] = (unsigned long long)(e);                                     \
+            }                                                                                      \
+        }                                                                                          \
+    } while (0)
 #else
+#define ITEM_T0() do {} while (0)
+#define ITEM_LOG(wid, type, e) do {} while (0)
 #define LSTAMP(idx) do {} while (0)
 #define WTIME(end) do {} while (0)
 #define PTIME(end) do {} while (0)
@@ -2013,6 +2035,7 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
             const int e = job_env(0, idx, incl);
+            ITEM_T0();
             WaveMT mt;
             uint32_t cellw;
             const int spst = J.c.bg ? claim_reset_mt(J.c, J.st, e, mt, lane, cellw)
@@ -2020,6 +2043,7 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
             if (J.c.diag && lane == 0 && (spst & 3) == SPAWN_READY) DIAG_ADD(g_spawn_hits);
             if (J.c.diag && lane == 0 && (spst & 3) == SPAWN_PARTIAL) DIAG_ADD(g_reset_part);
             do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, wid, spst, cellw, lane);
+            ITEM_LOG(wid, 2 - (spst & 3), e);
         } else if (!RO && idx < R + P) {
             if (J.c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
             else if (J.c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -2027,7 +2051,9 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
             const int j = idx - R;
             const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
             if (J.c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
+            ITEM_T0();
             do_spawn<MS, JL>(J.c, J.st, e, lds, wid, lane);
+            ITEM_LOG(wid, j < U ? 3 : 4, e);
         }
         int v = 0;
         if (lane == 0) v = atomicAdd(&qc[(kQClaim + x) * kQSpread], 1);
@@ -2360,6 +2386,9 @@ __global__ void __launch_bounds__(64) k_post(const KArgs)
     const int G = kargs().c.reset_slots, b = (int)blockIdx.x;
     if (b < G) {
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+#ifdef SNAKE_DIAG_ENC2   // (diagnostic: the second, encode-only launch, see launch_step)
+        if (kargs().aux) return;
+#endif
         autoreset_worker<MS, RO, JL>(b, G, lds);
     } else {
 #ifdef SNAKE_DIAG_NO_ENCODE   // (diagnostic build: instruction counts without the encodes)
@@ -2949,6 +2978,25 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     }
     t2.close();
     if ((rc = check_launch("k_post"))) return fail(rc);
+#ifdef SNAKE_DIAG_ENC2
+    // Diagnostic timing build: k_post once more with idle workers (aux set), so
+    // the encodes alone are timed ("k_encode") with the same launch shape, LDS
+    // and registers; they rewrite the same observations.
+    if (!k.lean) {
+        const int epw2 = k.enc_per_wave, n16 = k.ring_bytes >> 4;
+        const int npw = (k.fs * k.HW / 4 + kWave - 1) / kWave;
+        const int npf = k.tbl ? (npw <= 2 ? -2 : -8)
+                              : (epw2 <= 1 ? 0 : (n16 <= kWave ? 1 : (n16 <= 2 * kWave ? 2 : 8)));
+        const int enc_blocks = npf == 0 ? k.N : (k.N + epw2 - 1) / epw2;
+        const dim3 gp(k.reset_slots + enc_blocks);
+        const int lds_p = std::max(k.lds_bytes, k.tbl ? k.lds_tbl_bytes : k.lds_obs_bytes);
+        const KArgs a2{k, st, o, (const void *)1};
+        TimedLaunch t5("k_encode", sm);
+        if (k.link32) launch_post_s<false, 2>(k, a2, npf, gp, lds_p, sm);
+        else launch_post_s<false, 1>(k, a2, npf, gp, lds_p, sm);
+        t5.close();
+    }
+#endif
     return SNAKE_OK;
 }
 
@@ -3041,6 +3089,19 @@ extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, in
 #endif
 
 #ifdef SNAKE_STAMPS
+// out: the reset workers' items of the launches since the last call (4 words
+// each, see g_items), at most cap; returns their number
+extern "C" int snake_debug_items(unsigned long long *out, int cap)
+{
+    unsigned n = 0, z = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(snake::g_nitems), sizeof n) != hipSuccess) return -1;
+    n = std::min<unsigned>(n, (unsigned)std::min(cap, snake::kItems));
+    if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_items), sizeof(unsigned long long) * 4 * n) != hipSuccess)
+        return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(snake::g_nitems), &z, sizeof z) != hipSuccess) return -1;
+    return (int)n;
+}
+
 // out: 64 phase stamps of block 0, 2 * 8192 k_logic wave start/end realtimes,
 // 2 * 40960 k_post block start/end realtimes
 extern "C" int snake_debug_stamps(unsigned long long *out)

@@ -19,7 +19,8 @@ import numpy as np
 NONE, PARTIAL, READY = 0, 1, 2
 
 
-def simulate(trace, policy, windows, p_ok=1 / 1.105, seed=1):
+def simulate(trace, policy, windows, p_ok=1 / 1.105, seed=1, tries=None):
+    """tries(prod=..., am=...) -> attempts per job (default 1)"""
     T, N = trace.shape
     rng = np.random.default_rng(seed)
     status = np.full(N, READY, np.int8)
@@ -28,10 +29,11 @@ def simulate(trace, policy, windows, p_ok=1 / 1.105, seed=1):
     voids_ep = np.zeros(N, np.int32)
     acc = {w: dict(jobs=0, resets=0, hits=0, part=0, voids=0, steps=0) for w in windows}
     for t in range(T):
-        f = trace[t]
-        am = (f & 7).astype(np.int32)
+        f = trace[t].astype(np.int32)
+        am = f & 7
         drew = ((f >> 3) & 1).astype(bool)
-        mind = (f >> 4).astype(np.int32)
+        mind = (f >> 4) & 15
+        prod = (f >> 8) & 127
         end = am == 0
         eplen += 1
         hit = end & (status == READY)
@@ -42,13 +44,15 @@ def simulate(trace, policy, windows, p_ok=1 / 1.105, seed=1):
         since_void[void] = 0
         since_void[~void] += 1
         voids_ep[void] += 1
-        q = ~end & (status != READY) & policy(am=am, mind=mind, eplen=eplen, since_void=since_void,
+        q = ~end & (status != READY) & policy(am=am, mind=mind, prod=prod, eplen=eplen, since_void=since_void,
                                               voids_ep=voids_ep, drew=drew)
-        ok = rng.random(N) < p_ok
+        nt = tries(am=am, prod=prod) if tries is not None else 1
+        ok = rng.random(N) < 1 - (1 - p_ok) ** nt
         status[q & ok] = READY
         status[q & ~ok] = PARTIAL
         for (a, b), s in acc.items():
             if a <= t < b:
+                s['att'] = s.get('att', 0) + float((q * (1 + (nt > 1) * (1 - p_ok))).sum())
                 s['jobs'] += int(q.sum()); s['resets'] += int(end.sum()); s['hits'] += int(hit.sum())
                 s['part'] += int(part.sum()); s['voids'] += int(void.sum()); s['steps'] += 1
         eplen[end] = 0
@@ -59,7 +63,7 @@ def simulate(trace, policy, windows, p_ok=1 / 1.105, seed=1):
         n = max(s['steps'], 1)
         out[w] = dict(jobs=s['jobs'] / n, resets=s['resets'] / n, voids=s['voids'] / n,
                       hit=s['hits'] / max(s['resets'], 1), miss=(s['resets'] - s['hits'] - s['part']) / n,
-                      jps=s['jobs'] / max(s['hits'], 1))
+                      jps=s['jobs'] / max(s['hits'], 1), att=s.get('att', 0) / n)
     return out
 
 
