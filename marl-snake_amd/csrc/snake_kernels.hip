@@ -277,6 +277,9 @@ __device__ __forceinline__ int zero_bytes(uint32_t x)
 // Observation stores (the step's bulk output, 2/3 of its bytes) as
 // non-temporal stores: streamed past the caches, so they do not evict the env
 // state the next step's k_logic reads (cfg3 0.0929 -> 0.0908 ms, round 3).
+// (Round 5: write-back stores measured slower in the step -- cfg3 0.0846 ->
+// 0.0887 ms, cfg5 0.1019 -> 0.1184 -- although a lone store stream reaches
+// 5.3 TB/s with them against 4.5 TB/s non-temporal, scripts/microbench/storebw.hip.)
 template <typename T>
 __device__ __forceinline__ void obs_store(T *p, const T &v)
 {
@@ -684,6 +687,156 @@ __device__ void perm_trace(int S, const NP *link, const lu16 *jsmall, int (&q)[M
 #pragma unroll
     for (int k = 0; k < MS; k++) q[k] = bcast(x, k);
 }
+
+#ifdef SNAKE_DRAWBENCH
+// ------------------------------------------------ cooperative permutation draws
+// permutation(n)'s draws (the records of mt_perm_draws) on the kCoopW waves of
+// one workgroup: a round covers one aligned group of four key registers (256
+// raw words), wave w judging register 4g + w, instead of one wave's register
+// pair. The accept set is found by mt_perm_draws' bound refinement (accept iff
+// (w & mask) <= i - A_p, A_p = the accepts before word p), the prefix of the
+// counts of the waves before a wave exchanged through LDS once per refinement
+// pass: every wave writes its count, its open-word flag and the lane of the
+// bracket cut if its words hold it, one workgroup barrier, every wave reads all
+// four (two passes settle most rounds). Every wave holds the whole tempered key
+// (the twist runs on every wave: it is the same instructions, no latency lost)
+// and the round state i / mask / stream position, which all waves update the
+// same way from the exchanged counts. The waves of the workgroup must all call
+// it with the same MT state; they return with the same MT state and the
+// records written (the caller's barrier publishes them).
+// MEASURED SLOWER, kept for the diagnostic build only (scripts/attemptbench.py,
+// profiles/r05_attemptbench.json): identical records and poses, but a lone
+// attempt's draws take 2.1-2.5x the one-wave cycles (20x20, u16 record: 125 K
+// vs 42 K; 40x40: 356 K vs 144 K) -- a workgroup barrier and an LDS round trip
+// per refinement pass cost more than a whole one-wave round of ballots; with
+// k_post_lean's resets as four-wave groups (a reset without a record drawing
+// on all four) cfg5 went 0.1025 -> 0.1173 ms (profiles/r05_ab_coop_resets.jsonl).
+constexpr int kCoopW = 4;
+
+struct CoopXch {
+    uint4 *xb;   // LDS: [2][kCoopW] (ping-pong: a wave can be one exchange ahead)
+    int par;
+};
+
+// this wave's (cnt, und, cut) out, every wave's back (uniform values)
+__device__ __forceinline__ void coop_exch(CoopXch &x, int W, int cnt, int und, int cut, int (&ca)[kCoopW],
+                                          int (&ua)[kCoopW], int (&cuts)[kCoopW])
+{
+    uint4 *b = x.xb + x.par * kCoopW;
+    x.par ^= 1;
+    if ((threadIdx.x & (kWave - 1)) == 0) b[W] = make_uint4((uint32_t)cnt, (uint32_t)und, (uint32_t)cut, 0u);
+    // (LDS only: a workgroup fence would also drain the link-table atomics)
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < kCoopW; u++) {
+        const uint4 v = b[u];
+        ca[u] = __builtin_amdgcn_readfirstlane((int)v.x);
+        ua[u] = __builtin_amdgcn_readfirstlane((int)v.y);
+        cuts[u] = __builtin_amdgcn_readfirstlane((int)v.z);
+    }
+}
+
+template <typename NP>
+__device__ void mt_perm_draws_coop(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, uint4 *xbuf,
+                                   int W, int lane)
+{
+    int i = n - 1;
+    if (i < 1) return;
+    uint32_t mask = gen_mask((uint32_t)i);
+    int lo = (int)(mask >> 1) + 1;
+    constexpr int kBig = 0x3fffffff;
+    CoopXch x{xbuf, 0};
+    NP *dummy = link + link_n + lane;
+    uint32_t my[3];   // this wave's register of each four-register group, tempered
+    auto select_key = [&]() {
+#pragma unroll
+        for (int g = 0; g < 3; g++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int w = 0; w < kCoopW; w++)
+                if (4 * g + w < 10) v |= temper(m.w[4 * g + w]) & (0u - (uint32_t)(W == w));
+            my[g] = v;
+        }
+    };
+    select_key();
+    int ca[kCoopW], ua[kCoopW], cuts[kCoopW];
+    for (int guard = 0; i >= 1 && guard < (1 << 20); guard++) {
+        if (m.pos >= kMtN) {
+            mt_twist(m, lane);
+            select_key();
+        }
+#pragma unroll
+        for (int g = 0; g < 3; g++) {
+            // a round normally consumes the rest of the group; a bracket cut
+            // inside it repeats the group from the word after the cut
+            while (i >= 1 && m.pos < kMtN && (m.pos >> 8) == g) {
+                const int off = m.pos - 256 * g;                   // first unread word of the group
+                const int p = 64 * W + lane - off;                 // this word's offset in the round
+                const bool valid = p >= 0 && 256 * g + 64 * W + lane < kMtN;
+                const int v = valid ? (int)(my[g] & mask) : kBig;
+                // pass 0: the possible set; then alternate sure / possible sets
+                // from the other's prefix until they agree
+                unsigned long long c = __ballot(v <= i), a = 0ull;
+                const int k = i - lo + 1;                          // accepts left in this bracket
+                int cnt = __popcll(c);
+                coop_exch(x, W, cnt, 0, -1, ca, ua, cuts);
+                int bprev = 0;
+#pragma unroll
+                for (int u = 0; u < kCoopW; u++) bprev += (u < W) ? ca[u] : 0;
+                bool settled = false;
+                int b = 0;
+                for (int pass = 1; pass < 512 && !settled; pass++) {
+                    // the set from the previous pass gives this lane's prefix bound
+                    const unsigned long long prev = (pass & 1) ? c : a;
+                    b = mbcnt64(prev, bprev);
+                    const unsigned long long nw = __ballot(v + b <= i);
+                    if (pass & 1) a = nw; else c = nw;
+                    const int und = (a ^ c) != 0ull;
+                    cnt = __popcll(nw);
+                    // when this pass settles the round, nw == prev and bprev is
+                    // exact: the lane of the k-th accept of the round, if here
+                    int cut = -1;
+                    if (k - 1 - bprev >= 0 && k - 1 - bprev < cnt) {
+                        const unsigned long long hit = __ballot(inv_ballot(nw) && b == k - 1);
+                        cut = hit ? __ffsll((long long)hit) - 1 : -1;
+                    }
+                    coop_exch(x, W, cnt, und, cut, ca, ua, cuts);
+                    settled = (ua[0] | ua[1] | ua[2] | ua[3]) == 0;
+                    bprev = 0;
+#pragma unroll
+                    for (int u = 0; u < kCoopW; u++) bprev += (u < W) ? ca[u] : 0;
+                }
+                // a == c; b = the accepts before each word (bprev unchanged by the last pass)
+                int A = ca[0] + ca[1] + ca[2] + ca[3];
+                int wcut = kCoopW, lcut = 0;
+                const int end = min(256 * (g + 1), kMtN) - 256 * g;   // words of the group
+                int newoff = end;
+                if (A >= k) {   // the round ends right after the accept that leaves the bracket
+#pragma unroll
+                    for (int u = kCoopW - 1; u >= 0; u--)
+                        if (cuts[u] >= 0) { wcut = u; lcut = cuts[u]; }
+                    newoff = 64 * wcut + lcut + 1;
+                    A = k;
+                    if (W > wcut) a = 0ull;
+                    else if (W == wcut) a &= (2ull << lcut) - 1ull;
+                }
+                const int ii = i - b;
+                if constexpr (std::is_same<NP, lu16>::value) {
+                    *(inv_ballot(a) ? link + ii : dummy) = (uint16_t)v;
+                } else {
+                    if (inv_ballot(a)) perm_record(ii, v, S, link, jsmall);
+                }
+                m.pos = 256 * g + newoff;
+                i -= A;
+                mask = i > 0 ? (0xffffffffu >> __builtin_clz((uint32_t)i)) : 0u;
+                lo = (int)(mask >> 1) + 1;
+                if (newoff >= end) m.pos = min(256 * (g + 1), kMtN);
+            }
+        }
+    }
+}
+
+#endif  // SNAKE_DRAWBENCH
 
 // ------------------------------------------------------------ fruit respawn
 // random_empty_coords + grid[xs, ys] = FRUIT (grid_util.py:126-133,
@@ -1109,17 +1262,17 @@ __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &
 // over the frame stack. `mt` comes from load_reset_mt: with a ready spawn-ahead
 // record the poses are the record's and the draws are already done; a partial
 // record continues the retries where the record left them.
+// The rest of the reset once the spawn cells are known (lane's cell, lanes <
+// S*L): the grid, the snakes, the fruits, the records and the first observation.
+__device__ __forceinline__ void reset_paint(const KCfg &c, const snake_state &st, const snake_out &o, int e, WaveMT &mt, uint8_t *lds,
+                            int spw, int cell, bool failed, int lane);
+
 template <int MS, int JL>
 __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &o, int e,
                          WaveMT &mt, uint8_t *lds, int slot, int spw, uint32_t cellw, int lane)
 {
     const int spst = spw & 3;
-    uint8_t *frames = lds + c.lds_frames;
-    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
-    uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
-    uint8_t *work = frames + (c.fs - 1) * c.grid_stride;
-    const int S = c.S, L = c.L, W = c.W, SL = S * L;
-    const int sk = lane / L, si = lane - sk * L;
+    const int SL = c.S * c.L;
     int cell = -1;
     bool failed = false;
     if (spst == SPAWN_READY) {   // the record's cells (loaded with its key)
@@ -1135,6 +1288,19 @@ __device__ void do_reset(const KCfg &c, const snake_state &st, const snake_out &
             ok = spawn_attempt<MS, JL>(c, st, mt, lds, slot, q, cell, lane);
         failed = !ok;
     }
+    reset_paint(c, st, o, e, mt, lds, spw, cell, failed, lane);
+}
+
+__device__ __forceinline__ void reset_paint(const KCfg &c, const snake_state &st, const snake_out &o, int e, WaveMT &mt, uint8_t *lds,
+                            int spw, int cell, bool failed, int lane)
+{
+    const int spst = spw & 3;
+    uint8_t *frames = lds + c.lds_frames;
+    int *org = reinterpret_cast<int *>(lds + c.lds_centers);
+    uint16_t *fbuf = reinterpret_cast<uint16_t *>(lds + c.lds_fruit);
+    uint8_t *work = frames + (c.fs - 1) * c.grid_stride;
+    const int S = c.S, L = c.L, W = c.W, SL = S * L;
+    const int sk = lane / L, si = lane - sk * L;
     // make_grid (grid_util.py:14-20), then paint (:138-144)
     for (int x = lane; x < c.HW; x += kWave) {
         const int r = (int)__umulhi((uint32_t)x, c.mag_W), cc = x - r * W;   // x / W
@@ -3083,6 +3249,80 @@ __global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsi
 extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, int S, unsigned long long *out_dev)
 {
     hipLaunchKernelGGL(k_drawbench, dim3(1), dim3(64), 2 * n + 256, 0, mt_dev, pos0, n, S, out_dev);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+// One lone permutation attempt's draws (record cleared first where it needs
+// it) and trace: one wave (mt_perm_draws) or kCoopW waves (mt_perm_draws_coop),
+// the record kind JL as in spawn_attempt (1 u16 record, 2 u32 link table in
+// LDS, 0 u32 link table in global memory `gl`).
+// out: [cycles to the end of the draws, trace cycles, final MT position, arr[0..S)]
+template <bool COOP, int JL>
+__global__ void k_attemptbench(const uint32_t *mt_src, int pos0, int n, int S, uint32_t *gl, unsigned long long *out)
+{
+    using namespace snake;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x & (kWave - 1), W = (int)(threadIdx.x >> 6);
+    uint4 *xb = reinterpret_cast<uint4 *>(lds);          // exchange slots
+    lu16 *jsmall = (lu16 *)(lds + 128);                   // S entries
+    uint8_t *rec = lds + 256;
+    const int stride = (n + 3) / 4 * 4 + kWave;           // (KCfg.link_stride)
+    WaveMT mt;
+    mt_load(mt, mt_src, pos0, lane);
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    if constexpr (JL == 1) {
+        lu16 *jarr = (lu16 *)rec;
+        if (COOP) mt_perm_draws_coop(mt, n, S, jarr, n, jarr, xb, W, lane);
+        else mt_perm_draws(mt, n, S, jarr, n, jarr, lane);
+    } else if constexpr (JL == 2) {
+        lu32 *link = (lu32 *)rec;
+        for (int x = 4 * threadIdx.x; x < stride - kWave; x += 4 * blockDim.x) *(lu4 *)(link + x) = (v4u32)kNoLink;
+        __syncthreads();
+        if (COOP) mt_perm_draws_coop(mt, n, S, link, n, jsmall, xb, W, lane);
+        else mt_perm_draws(mt, n, S, link, n, jsmall, lane);
+    } else {
+        gu32 *link = (gu32 *)gl;
+        for (int x = 4 * threadIdx.x; x < stride - kWave; x += 4 * blockDim.x) *(gu4 *)(link + x) = (v4u32)kNoLink;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        __syncthreads();
+        if (COOP) mt_perm_draws_coop(mt, n, S, link, n, jsmall, xb, W, lane);
+        else mt_perm_draws(mt, n, S, link, n, jsmall, lane);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    }
+    __syncthreads();
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (W != 0) return;
+    int q[4];
+    if constexpr (JL == 1) perm_trace_j<4>(S, n, (const lu16 *)rec, q, lane);
+    else if constexpr (JL == 2) perm_trace<4>(S, (const lu32 *)rec, jsmall, q, lane);
+    else perm_trace<4>(S, (const gu32 *)gl, jsmall, q, lane);
+    wave_sync();
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+        out[0] = t1 - t0; out[1] = t2 - t1; out[2] = (unsigned long long)mt.pos;
+        for (int k = 0; k < 4; k++) out[3 + k] = (unsigned long long)q[k];
+    }
+}
+
+// coop: 0 one wave, 1 kCoopW waves; jl: 0/1/2; gl_dev: (n + 68) u32 for jl 0
+extern "C" int snake_debug_attemptbench(const uint32_t *mt_dev, int pos0, int n, int S, int coop, int jl,
+                                        uint32_t *gl_dev, unsigned long long *out_dev)
+{
+    using namespace snake;
+    if (S > 4) return -1;
+    const int stride = (n + 3) / 4 * 4 + kWave;
+    const int lds = 256 + (jl == 1 ? 2 * (n + kWave) : (jl == 2 ? 4 * stride : 0));
+    const dim3 g(1), b(coop ? kWave * kCoopW : kWave);
+    if (coop) {
+        if (jl == 1) hipLaunchKernelGGL((k_attemptbench<true, 1>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        else if (jl == 2) hipLaunchKernelGGL((k_attemptbench<true, 2>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        else hipLaunchKernelGGL((k_attemptbench<true, 0>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+    } else {
+        if (jl == 1) hipLaunchKernelGGL((k_attemptbench<false, 1>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        else if (jl == 2) hipLaunchKernelGGL((k_attemptbench<false, 2>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        else hipLaunchKernelGGL((k_attemptbench<false, 0>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+    }
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
