@@ -16,6 +16,10 @@
 
 #include "snake_internal.h"
 
+#ifndef SNAKE_SPAWN_PRIO_SMALL   // (A/B builds: scripts/build_variants.sh)
+#define SNAKE_SPAWN_PRIO_SMALL 3
+#endif
+
 namespace snake {
 
 static thread_local char g_err[512];
@@ -464,9 +468,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
     const bool bg = bg_of(c, n_cand);
     // spawn-ahead jobs at 1, below the encodes; small batches with in-step
-    // spawn-ahead at 3 (a lone attempt is there the step's critical path: cfg2
-    // 0.0510 -> 0.0494 ms; at cfg3 it costs 0.0905 -> 0.0960)
-    k->spawn_prio = N <= 32768 && !bg ? 3 : 1;   // (round 4, with the LDS link table: cfg4 0.0595 -> 0.0584 ms)
+    // spawn-ahead higher (a lone attempt is there the step's critical path:
+    // cfg2 0.0510 -> 0.0494 ms; at cfg3 it costs 0.0905 -> 0.0960). Until round
+    // 5 the workers mapped every value >= 2 to s_setprio 2, the encodes' level
+    // (ADVICE r4): round 4's "priority 3" (cfg4 0.0595 -> 0.0584 ms) ran at 2.
+    k->spawn_prio = N <= 32768 && !bg ? SNAKE_SPAWN_PRIO_SMALL : 1;
     // the encodes above the spawn-ahead jobs: the bandwidth-bound encodes then
     // keep HBM busy while the compute-bound workers fill the issue gaps (cfg3
     // 0.1275 -> 0.1200 ms against the hardware default 0). With background

@@ -44,6 +44,8 @@ __device__ unsigned long long g_spawn_hits[kDiagSlots * kDiagSpread];   // auto-
 __device__ unsigned long long g_spawn_jobs[kDiagSlots * kDiagSpread];   // spawn-ahead jobs dequeued
 __device__ unsigned long long g_spawn_void[kDiagSlots * kDiagSpread];   // ready records voided by a fruit draw
 __device__ unsigned long long g_reset_part[kDiagSlots * kDiagSpread];   // auto-resets that found a partial record
+__device__ unsigned long long g_resp_slow[kDiagSlots * kDiagSpread];    // k_logic respawns on the full-wave path (no room)
+__device__ unsigned long long g_resp_slow2[kDiagSlots * kDiagSpread];   // ... (room, too few accepts among the prefetched raws)
 #define DIAG_ADD(arr) atomicAdd(&(arr)[(blockIdx.x % kDiagSlots) * kDiagSpread], 1ull)
 
 #ifdef SNAKE_STAMPS
@@ -61,14 +63,19 @@ __device__ unsigned long long g_posttime[2 * kPostTimes];   // k_post: every blo
             g_posttime[2 * blockIdx.x + (end)] = __builtin_amdgcn_s_memrealtime(); \
         __builtin_amdgcn_sched_barrier(0);                                         \
     } while (0)
+// (and every k_logic wave's s_memrealtime at each phase: g_wphase[wave][idx - 40])
+__device__ unsigned long long g_wphase[16 * kWaveTimes];
 #define LSTAMP(idx)                                                                \
     do {                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                         \
         if (blockIdx.x == 0) {                                                     \
-            __builtin_amdgcn_sched_barrier(0);                                     \
             unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
             if (threadIdx.x == 0) g_stamps[idx] = _t;                              \
-            __builtin_amdgcn_sched_barrier(0);                                     \
         }                                                                          \
+        const unsigned _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  \
+        if ((threadIdx.x & 63) == 0 && _w < kWaveTimes)                            \
+            g_wphase[16 * _w + (idx) - 40] = __builtin_amdgcn_s_memrealtime();     \
+        __builtin_amdgcn_sched_barrier(0);                                         \
     } while (0)
 #define WTIME(end)                                                                 \
     do {                                                                           \
@@ -1882,6 +1889,10 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     // the rest (a twist needed, or too few accepts among the prefetched raws), one
     // env at a time with the whole wave
     unsigned long long fm = __ballot(need && !fast_done && k == 0);
+    if (c.diag && need && !fast_done && k == 0) {
+        if (!room) DIAG_ADD(g_resp_slow);
+        else DIAG_ADD(g_resp_slow2);
+    }
     while (fm) {
         const int L = __ffsll((long long)fm) - 1;
         fm &= fm - 1;
@@ -2211,9 +2222,10 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
             do_reset<MS, JL>(J.c, J.st, J.o, e, mt, lds, wid, spst, cellw, lane);
             ITEM_LOG(wid, 2 - (spst & 3), e);
         } else if (!RO && idx < R + P) {
-            if (J.c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);
+            if (J.c.spawn_prio == 0) __builtin_amdgcn_s_setprio(0);   // (s_setprio takes an immediate)
             else if (J.c.spawn_prio == 1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(2);
+            else if (J.c.spawn_prio == 2) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(3);
             const int j = idx - R;
             const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
             if (J.c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
@@ -3052,11 +3064,20 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     int rc = check_launch("k_logic");
     if (rc) return rc;
     // From here on k_logic has filled this step's queue set: a failure zeroes
-    // its counters, so the next step does not run this step's queues.
+    // its counters, so the next step does not run this step's queues. Once
+    // k_spawn is launched it owns the set's spawn counters (it reads them and
+    // re-zeroes them at its end): only the reset counters are zeroed
+    // then -- queue 0's shard counts and the claim / done counters.
+    bool spawn_launched = false;
     auto fail = [&](int r) {
         int *qc = st.resetq + (int64_t)k.qpar * (kNumQ * kQShards * k.q_cap + kQCounters) +
                   kNumQ * kQShards * k.q_cap;
-        (void)hipMemsetAsync(qc, 0, sizeof(int) * kQSpGen * kQSpread, sm);   // (not the finished count)
+        if (!spawn_launched) {
+            (void)hipMemsetAsync(qc, 0, sizeof(int) * kQSpGen * kQSpread, sm);   // (not the finished count)
+        } else {
+            (void)hipMemsetAsync(qc, 0, sizeof(int) * kQShards * kQSpread, sm);
+            (void)hipMemsetAsync(qc + kQClaim * kQSpread, 0, sizeof(int) * (kQDone + 1 - kQClaim) * kQSpread, sm);
+        }
         return r;
     };
     const KArgs a{k, st, o, nullptr};
@@ -3095,13 +3116,16 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bgc->x, sa);
         t4.close();
         if ((rc = check_launch("k_spawn"))) return fail(rc);
+        // (counted as soon as it is launched: its last worker adds one to the
+        // set's finished count whatever fails after this point)
+        spawn_launched = true;
+        bgc->launched[k.qpar]++;
+        bgc->steps++;
         if (hipEventRecord(bgc->done[k.qpar], bgc->x) != hipSuccess) {
             set_error("background spawn event failed");
             return fail(SNAKE_E_LAUNCH);
         }
         bgc->pending[k.qpar] = true;
-        bgc->launched[k.qpar]++;
-        bgc->steps++;
     }
     TimedLaunch t2("k_post", sm);
     if (k.lean) {
@@ -3187,7 +3211,9 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
                     : !strcmp(kernel, "spawn_hits") ? (const void *)snake::g_spawn_hits
                     : !strcmp(kernel, "spawn_jobs") ? (const void *)snake::g_spawn_jobs
                     : !strcmp(kernel, "spawn_void") ? (const void *)snake::g_spawn_void
-                    : !strcmp(kernel, "reset_partial") ? (const void *)snake::g_reset_part : nullptr;
+                    : !strcmp(kernel, "reset_partial") ? (const void *)snake::g_reset_part
+                    : !strcmp(kernel, "respawn_slow") ? (const void *)snake::g_resp_slow
+                    : !strcmp(kernel, "respawn_slow2") ? (const void *)snake::g_resp_slow2 : nullptr;
     if (sym) {
         const int n = one ? 1 : snake::kDiagSlots * snake::kDiagSpread;
         std::vector<unsigned long long> v(n, 0ull), z(n, 0ull);
@@ -3329,6 +3355,13 @@ extern "C" int snake_debug_attemptbench(const uint32_t *mt_dev, int pos0, int n,
 #endif
 
 #ifdef SNAKE_STAMPS
+// out: 16 * 8192 per-wave phase realtimes of the last k_logic (g_wphase)
+extern "C" int snake_debug_wphase(unsigned long long *out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_wphase), sizeof(unsigned long long) * 16 * snake::kWaveTimes) ==
+                   hipSuccess ? 0 : -1;
+}
+
 // out: the reset workers' items of the launches since the last call (4 words
 // each, see g_items), at most cap; returns their number
 extern "C" int snake_debug_items(unsigned long long *out, int cap)

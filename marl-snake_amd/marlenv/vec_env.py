@@ -74,6 +74,7 @@ class _StepInfo(dict):
             return env._view(slab, 'err')
         ended = self['episode_done'].view(-1, 1)
         torch = _torch()
+        st = None
         if _raw_stream(env._dev_index) == self._stream:
             ctx = torch.cuda.device(env.device)           # (already the step's stream)
         else:
@@ -82,10 +83,21 @@ class _StepInfo(dict):
             ctx = torch.cuda.stream(st)
         with ctx:
             if k == 'rank':
-                return env._view(slab, 'rank').masked_fill(~ended, 0)
-            if self._es is None:
-                self._es = env._view(slab, 'ep_stats').masked_fill(~ended.view(-1, 1, 1), 0.0)
-        return self._es[:, ('episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills').index(k)]
+                out = env._view(slab, 'rank').masked_fill(~ended, 0)
+            else:
+                if self._es is None:
+                    self._es = env._view(slab, 'ep_stats').masked_fill(~ended.view(-1, 1, 1), 0.0)
+                out = self._es
+        if st is not None:
+            # filled on the step's stream, read on the caller's current one: that
+            # stream waits for the fill, and the allocator keeps the block until
+            # the current stream's work on it is done
+            cur = torch.cuda.current_stream(env.device)
+            cur.wait_stream(st)
+            out.record_stream(cur)
+        if k == 'rank':
+            return out
+        return out[:, ('episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills').index(k)]
 
     def __getitem__(self, k):
         v = dict.__getitem__(self, k)

@@ -693,3 +693,70 @@ def test_full_size_cfg5_sampled(oracle):
         assert int(heads[~alive].sum()) == 0
         assert not bool(info['error'].any())
     assert n_ep > 0
+
+
+def test_background_state_lifetime():
+    """snake_release / SnakeVecEnv.close() on a background spawn-ahead board
+    (40x40, 8 snakes: k_spawn on the library's per-state stream): closing twice
+    is harmless, and an env created afterwards -- its state buffers likely at
+    the freed addresses, which key the library's background context -- rolls
+    out bit-identically to a twin that lived beside it throughout, with its
+    spawn-ahead records still served (a stale context's launch count would
+    leave the device-side queue gate shut: identical results, no hits)."""
+    from marlenv import SnakeVecEnv, _native
+    N, S = 512, 8
+    kw = dict(height=40, width=40, vision_range=5, frame_stack=2)
+    twin = SnakeVecEnv(N, num_snakes=S, seed=5, **kw)
+    a = SnakeVecEnv(N, num_snakes=S, seed=9, **kw)
+    a.reset()
+    g = torch.Generator(device='cuda').manual_seed(3)
+    for _ in range(30):
+        a.step(torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8))
+    freed = {a.env_rec.data_ptr(), a.mt.data_ptr(), a.grid.data_ptr()}
+    a.close()
+    a.close()
+    del a
+    b = SnakeVecEnv(N, num_snakes=S, seed=5, **kw)
+    reused = bool(freed & {b.env_rec.data_ptr(), b.mt.data_ptr(), b.grid.data_ptr()})
+    assert torch.equal(b.reset(), twin.reset())
+    for k in ('spawn_hits', 'spawn_jobs'):
+        _native.timing_read(k)
+    hits = 0
+    for t in range(120):
+        act = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        _native.timing_enable(True)
+        ob, rb, db, ib = b.step(act)
+        _native.timing_enable(False)
+        hits += _native.timing_read('spawn_hits')[1]
+        ot, rt, dt, it = twin.step(act)
+        assert torch.equal(ob, ot) and torch.equal(rb, rt) and torch.equal(db, dt), f'step {t}'
+        assert torch.equal(ib['episode_done'], it['episode_done']), f'step {t}'
+    assert torch.equal(b.grids(), twin.grids())
+    assert hits > 0, f'no spawn-ahead hits after the re-created state (addresses reused: {reused})'
+    b.close()
+    twin.close()
+
+
+def test_info_read_on_another_stream():
+    """The episode summary is filled on the stream the step ran on; read from
+    another stream it is ordered after that fill: the values equal
+    the ones read on the step's own stream."""
+    from marlenv import SnakeVecEnv
+    N, S = 256, 4
+    v = SnakeVecEnv(N, num_snakes=S, seed=2, height=10, width=10)
+    w = SnakeVecEnv(N, num_snakes=S, seed=2, height=10, width=10)
+    v.reset(), w.reset()
+    side = torch.cuda.Stream()
+    g = torch.Generator(device='cuda').manual_seed(5)
+    seen = 0
+    for t in range(60):
+        a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            _, _, _, iv = v.step(a)
+        _, _, _, iw = w.step(a)
+        # read v's info on the default stream (not the one it was stepped on)
+        for k in ('rank', 'episode_scores', 'episode_steps', 'episode_fruits', 'episode_kills'):
+            assert torch.equal(iv[k], iw[k]), (t, k)
+        seen += int(iw['episode_done'].sum())
+    assert seen > 0
