@@ -1673,6 +1673,9 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     // needs old[j], old[j+1] and old[j+397] only): the twist is left pending in
     // the stored position (> 624), every MT consumer applies it
     const bool room = mtpos + G * kRespawnT <= kMtN + 226;
+    // (issued for every env right after the staging instead, before the rules
+    // say which envs eat: cfg3 k_logic 24.0 -> 26.0 us, cfg4 20.0 -> 19.4,
+    // round 5, profiles/r05_ab_raw_early.jsonl)
     uint32_t raws[kRespawnT];
     {
         const uint32_t *key = st.mt + (int64_t)e * kMtN;
