@@ -74,7 +74,8 @@ typedef struct {
                                                          (> 624: the key's twist is pending, position
                                                          624 + j = word j of the next key),
                                                          spawn-ahead status word (bits 0-1: 0 none,
-                                                         1 partial, 2 ready; bit 2: which of the env's two
+                                                         1 partial, 2 ready, 3 being drawn by a background
+                                                         job; bit 2: which of the env's two
                                                          records holds it (background spawn-ahead); bits
                                                          3-31: the record's generation),
                                                          spawn failure (1: the last reset gave up, below);

@@ -51,7 +51,9 @@ enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, 
 // spawn-ahead status word (env word ENV_SPAWN): bits 0-1 the status, bit 2 the
 // record buffer holding the record (background spawn-ahead keeps two per env),
 // bits 3-31 the record's generation (bumped by every MT draw that voids it)
-enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2 };
+// DRAWING (background spawn-ahead only): a k_spawn job is drawing the record
+// (from the env's own MT state or the partial record the buffer bit points at)
+enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2, SPAWN_DRAWING = 3 };
 
 // Everything a kernel needs, by value (a kernel argument).
 struct KCfg {

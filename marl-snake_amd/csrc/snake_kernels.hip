@@ -46,6 +46,8 @@ __device__ unsigned long long g_spawn_void[kDiagSlots * kDiagSpread];   // ready
 __device__ unsigned long long g_reset_part[kDiagSlots * kDiagSpread];   // auto-resets that found a partial record
 __device__ unsigned long long g_resp_slow[kDiagSlots * kDiagSpread];    // k_logic respawns on the full-wave path (no room)
 __device__ unsigned long long g_resp_slow2[kDiagSlots * kDiagSpread];   // ... (room, too few accepts among the prefetched raws)
+__device__ unsigned long long g_gate_shut[kDiagSlots * kDiagSpread];    // k_logic waves that found the background queue set busy
+__device__ unsigned long long g_draw_wait[kDiagSlots * kDiagSpread];    // resets that waited for a background job (DRAWING)
 #define DIAG_ADD(arr) atomicAdd(&(arr)[(blockIdx.x % kDiagSlots) * kDiagSpread], 1ull)
 
 #ifdef SNAKE_STAMPS
@@ -1245,12 +1247,31 @@ __device__ __forceinline__ int load_reset_mt(const KCfg &c, const snake_state &s
 // Background spawn-ahead (KCfg.bg): an auto-reset takes env e's record with one
 // atomic that bumps the generation (a k_spawn job still working on the env then
 // fails its publish), and reads the record it found with sc1 loads.
+// A reset that finds a background job drawing the env's record right now
+// (status SPAWN_DRAWING, set by do_spawn_bg) waits for the job to publish
+// instead of voiding it and drawing the same permutations again inline: the
+// job was queued at least a step earlier and is usually close to done, while an
+// inline 40x40 attempt took ~70-80 us of k_post_lean's span in a quarter of
+// cfg5's steps (round 5 kernel trace). The wait is bounded (kDrawWait ticks of
+// the 100 MHz clock, far beyond a job's ~100 us); after it the claim voids the
+// job as before and the reset draws from the env's own state -- right for a job
+// that started from a partial record too: the env's state is where that
+// record's failed permutations began, so the reset replays them.
+constexpr unsigned long long kDrawWait = 200000;   // 2 ms
 __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &st, int64_t e, WaveMT &mt,
                                               int lane, uint32_t &cellw)
 {
     int v = 0;
-    if (lane == 0) v = (int)atomicAdd(reinterpret_cast<uint32_t *>(st.env + e * kEnvRec + ENV_SPAWN), kGenOne);
-    const int spw = __shfl(v, 0);
+    if (lane == 0) {
+        uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + e * kEnvRec + ENV_SPAWN);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        if (c.diag && (ld_sc1(wp) & 3u) == SPAWN_DRAWING) DIAG_ADD(g_draw_wait);
+        while ((ld_sc1(wp) & 3u) == SPAWN_DRAWING && __builtin_amdgcn_s_memrealtime() - t0 < kDrawWait)
+            __builtin_amdgcn_s_sleep(8);
+        v = (int)atomicAdd(wp, kGenOne);
+    }
+    int spw = __shfl(v, 0);
+    if ((spw & 3) == SPAWN_DRAWING) spw &= ~3;   // (still drawing: from the env's own state, as for NONE)
     cellw = 0;
     if ((spw & 3) != SPAWN_NONE) {
         const uint32_t *rec = spawn_rec(c, st, e, (spw >> 2) & 1);
@@ -1646,8 +1667,9 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     const bool urgent = __popc(am) <= 1;
     // (background: only into a queue set its spawn kernels have finished with)
     const bool set_free = !BG || (uint32_t)bcast((int)in.gate, 0) == c.spawn_gate;
+    if (BG && c.diag && !set_free && lane == 0) DIAG_ADD(g_gate_shut);
     const bool spawn_q = c.spawn_thr >= 0 && set_free && env_ok && !bad && !ep_end &&
-                         (need ? true : spst != SPAWN_READY) && __popc(am) <= c.spawn_thr;
+                         (need ? true : spst < SPAWN_READY) && __popc(am) <= c.spawn_thr;   // (DRAWING: a job has it)
     const unsigned long long pm = __ballot(spawn_q && urgent && k == 0);
     const unsigned long long pn = __ballot(spawn_q && !urgent && k == 0);
     int pbase = 0, nbase = 0;
@@ -2097,11 +2119,23 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
     uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN);
     int v = 0;
     if (lane == 0) v = (int)atomicAdd(wp, 0u);   // (the memory-side value)
-    const uint32_t spw = (uint32_t)__shfl(v, 0);
-    if (((spw >> 3) & ((1u << kQGenBits) - 1u)) != qgen || (spw & 3u) == SPAWN_READY) return;
+    uint32_t spw = (uint32_t)__shfl(v, 0);
+    // (READY: nothing to do; DRAWING: another job -- an earlier step's -- has it)
+    if (((spw >> 3) & ((1u << kQGenBits) - 1u)) != qgen || (spw & 3u) >= SPAWN_READY) return;
+    const uint32_t st0 = spw & 3u;
+    {
+        // mark the record as being drawn: claim_reset_mt waits for it, and a job
+        // of the other queue set's kernel (they may overlap) leaves the env
+        // alone. A word that moved meanwhile (a draw voided it, a reset claimed
+        // it, the other job took it) ends this job.
+        int won = 0;
+        if (lane == 0) won = atomicCAS(wp, spw, (spw & ~3u) | SPAWN_DRAWING) == spw ? 1 : 0;
+        if (!__shfl(won, 0)) return;
+        spw = (spw & ~3u) | SPAWN_DRAWING;
+    }
     const int buf = (spw >> 2) & 1;
     WaveMT mt;
-    if ((spw & 3u) != SPAWN_NONE) {
+    if (st0 != SPAWN_NONE) {
         const uint32_t *rec = spawn_rec(c, st, e, buf);
         mt_load_sc1(mt, rec, (int)ld_sc1(rec + kSpawnPos), lane);
     } else {
@@ -2665,6 +2699,7 @@ __device__ __forceinline__ void encode_lean_block(const KCfg &c, const snake_sta
 template <int MS, bool RO, bool TBL>
 __global__ void __launch_bounds__(256) k_post_lean(const KArgs)
 {
+    PTIME(0);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int G = kargs().c.reset_slots, GB = (G + 3) >> 2, b = (int)blockIdx.x;
     if (b < GB) {
@@ -2675,6 +2710,7 @@ __global__ void __launch_bounds__(256) k_post_lean(const KArgs)
         if constexpr (TBL) encode_tbl_block<8, 256>(A.c, A.st, A.o, b - GB);
         else encode_lean_block<8, 256>(A.c, A.st, A.o, b - GB);
     }
+    PTIME(1);
 }
 
 template <int MS, int JL>
@@ -2860,8 +2896,13 @@ constexpr unsigned kJoinFlags = hipEventDisableTiming | hipEventDisableSystemFen
 // (k_spawn's start), the event recorded after the last k_spawn of each queue
 // set, the step counter whose parity picks the queue set. Created by the
 // state's first step, destroyed by snake_release.
+// One background stream per queue set (round 5): a set's k_spawn only waits for
+// that set's previous one, so consecutive steps' spawn kernels may overlap --
+// with one stream they queued behind each other (a 40x40 job takes about a
+// step) and k_logic found its set's previous kernel unfinished in ~21 % of
+// cfg5's steps, queued nothing, and the next step's resets drew inline.
 struct BgCtx {
-    hipStream_t x = nullptr;
+    hipStream_t x[2] = {nullptr, nullptr};
     hipEvent_t fork = nullptr;
     hipEvent_t done[2] = {nullptr, nullptr};
     uint64_t steps = 0;
@@ -2873,10 +2914,12 @@ static std::map<const void *, BgCtx> g_bg;
 
 static void destroy_bg(BgCtx &c)
 {
-    if (c.x) (void)hipStreamSynchronize(c.x);   // (its last k_spawn)
+    for (hipStream_t x : c.x)
+        if (x) (void)hipStreamSynchronize(x);   // (its last k_spawn)
     for (hipEvent_t ev : {c.fork, c.done[0], c.done[1]})
         if (ev) (void)hipEventDestroy(ev);
-    if (c.x) (void)hipStreamDestroy(c.x);
+    for (hipStream_t x : c.x)
+        if (x) (void)hipStreamDestroy(x);
     c = BgCtx();
 }
 
@@ -2887,7 +2930,8 @@ static BgCtx *bg_ctx(const snake_state &st, bool create)
     if (it != g_bg.end()) return &it->second;
     if (!create) return nullptr;
     BgCtx c;
-    if (hipStreamCreateWithFlags(&c.x, hipStreamNonBlocking) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&c.x[0], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c.x[1], hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c.fork, kJoinFlags) != hipSuccess ||
         hipEventCreateWithFlags(&c.done[0], kJoinFlags) != hipSuccess ||
         hipEventCreateWithFlags(&c.done[1], kJoinFlags) != hipSuccess) {
@@ -2924,7 +2968,7 @@ int release_background(const snake_state &st)
         c = it->second;
         g_bg.erase(it);
     }
-    DeviceGuard dg(c.x);   // (the stream's device current while it is destroyed)
+    DeviceGuard dg(c.x[0]);   // (the streams' device current while they are destroyed)
     destroy_bg(c);
     return dg.dev < 0 ? SNAKE_E_LAUNCH : SNAKE_OK;
 }
@@ -3104,7 +3148,8 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     if (bgc) {
         // this step's spawn kernel on the background stream once k_logic has
         // passed; not joined (the k_logic two steps later waits for it)
-        if (hipEventRecord(bgc->fork, sm) != hipSuccess || hipStreamWaitEvent(bgc->x, bgc->fork, 0) != hipSuccess) {
+        hipStream_t bx = bgc->x[k.qpar];
+        if (hipEventRecord(bgc->fork, sm) != hipSuccess || hipStreamWaitEvent(bx, bgc->fork, 0) != hipSuccess) {
             set_error("fork to the background stream failed");
             return fail(SNAKE_E_LAUNCH);
         }
@@ -3112,11 +3157,11 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         ks.lds_link = 0;   // (only the draw record)
         const int lds_sp = (int)(((int64_t)2 * (k.n_cand + kWave) + 15) / 16 * 16);
         const dim3 gs(k.spawn_slots);
-        TimedLaunch t4("k_spawn", bgc->x);
+        TimedLaunch t4("k_spawn", bx);
         const KArgs sa{ks, st, o, nullptr};
-        if (k.S <= 4) hipLaunchKernelGGL(k_spawn<4>, gs, block, lds_sp, bgc->x, sa);
-        else if (k.S <= 8) hipLaunchKernelGGL(k_spawn<8>, gs, block, lds_sp, bgc->x, sa);
-        else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bgc->x, sa);
+        if (k.S <= 4) hipLaunchKernelGGL(k_spawn<4>, gs, block, lds_sp, bx, sa);
+        else if (k.S <= 8) hipLaunchKernelGGL(k_spawn<8>, gs, block, lds_sp, bx, sa);
+        else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bx, sa);
         t4.close();
         if ((rc = check_launch("k_spawn"))) return fail(rc);
         // (counted as soon as it is launched: its last worker adds one to the
@@ -3124,7 +3169,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         spawn_launched = true;
         bgc->launched[k.qpar]++;
         bgc->steps++;
-        if (hipEventRecord(bgc->done[k.qpar], bgc->x) != hipSuccess) {
+        if (hipEventRecord(bgc->done[k.qpar], bx) != hipSuccess) {
             set_error("background spawn event failed");
             return fail(SNAKE_E_LAUNCH);
         }
@@ -3216,7 +3261,9 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
                     : !strcmp(kernel, "spawn_void") ? (const void *)snake::g_spawn_void
                     : !strcmp(kernel, "reset_partial") ? (const void *)snake::g_reset_part
                     : !strcmp(kernel, "respawn_slow") ? (const void *)snake::g_resp_slow
-                    : !strcmp(kernel, "respawn_slow2") ? (const void *)snake::g_resp_slow2 : nullptr;
+                    : !strcmp(kernel, "respawn_slow2") ? (const void *)snake::g_resp_slow2
+                    : !strcmp(kernel, "gate_shut") ? (const void *)snake::g_gate_shut
+                    : !strcmp(kernel, "draw_wait") ? (const void *)snake::g_draw_wait : nullptr;
     if (sym) {
         const int n = one ? 1 : snake::kDiagSlots * snake::kDiagSpread;
         std::vector<unsigned long long> v(n, 0ull), z(n, 0ull);

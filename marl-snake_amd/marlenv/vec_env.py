@@ -18,6 +18,7 @@ reproduces gym 0.23.1's worker that make_snake actually runs (wrappers.py:212):
 every env is reset after every step (rewards/dones/info of the step, the reset obs).
 """
 import ctypes
+import sys
 
 import numpy as np
 
@@ -43,8 +44,8 @@ def _current_device():
 
 
 def torch_cuda_alive():
-    """False during interpreter shutdown (no library calls from finalizers then)."""
-    import sys
+    """False during interpreter shutdown (no library calls from finalizers then;
+    `sys` is the module-level binding: an import there fails once meta_path is gone)."""
     return not sys.is_finalizing()
 
 

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Collect one scripts/r04_profiles.sh run into profiles/: the bench lines, the
+"""Collect one scripts/profile_set.sh run into profiles/: the bench lines, the
 rocprofv3 kernel-stats summaries per config, PMC HBM traffic (FETCH_SIZE x2 +
-WRITE_SIZE, scripts/pmc_summary.py) and SQ counters per launch.
+WRITE_SIZE, scripts/pmc_summary.py), SQ counters per launch and the spawn-ahead
+counters.
 
-    python scripts/r04_collect.py gpurun_out/r04final --tag r04
+    python scripts/collect_set.py gpurun_out/r05 --tag r05
 """
 import argparse
 import csv
@@ -28,10 +29,10 @@ def last_json(path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('run')
-    ap.add_argument('--tag', default='r04')
+    ap.add_argument('--tag', required=True)
     a = ap.parse_args()
     prof = os.path.join(ROOT, 'profiles')
-    lines = {'note': f'scripts/r04_profiles.sh on one MI355X ({a.run}); bench_<cfg>: --steps 2000 --warmup 200; '
+    lines = {'note': f'scripts/profile_set.sh on one MI355X ({a.run}); bench_<cfg>: --steps 2000 --warmup 200; '
                      'driverwin: the driver\'s --steps 20 --warmup 5 with the CPU baseline'}
     for name in sorted(os.listdir(a.run)):
         m = re.match(r'(bench_\w+|driverwin)\.log$', name)
@@ -84,6 +85,10 @@ def main():
         with open(os.path.join(prof, fn), 'w') as fh:
             json.dump(obj, fh, indent=1)
             fh.write('\n')
+    cnt = os.path.join(a.run, 'counters.log')
+    if os.path.exists(cnt):   # (scripts/spawn_counters.py's lines only)
+        with open(os.path.join(prof, f'{a.tag}_spawn_counters.txt'), 'w') as fh:
+            fh.writelines(x for x in open(cnt) if x.startswith('cfg'))
     # the bench line's dominant-kernel average against rocprof's
     for c, ln in lines.items():
         if isinstance(ln, dict) and c.startswith('bench_'):

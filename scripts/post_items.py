@@ -56,8 +56,8 @@ def main():
     acts = torch.randint(0, 3, (a.skip + a.steps, N, S), generator=g, device='cuda', dtype=torch.int8)
     buf = np.zeros(64 + 2 * KWT + 2 * KPT, np.uint64)
     items = np.zeros(4 * KIT, np.uint64)
-    G = min(N, 2048)
-    spans, enc_ends, crit, encs = [], [], Counter(), []
+    G = min(N, 2048) // (4 if a.cfg == 'cfg5' else 1)   # worker blocks (k_post_lean: four workers each)
+    spans, enc_ends, crit, encs, gaps, lspan = [], [], Counter(), [], [], []
     per = {t: dict(n=[], dur=[], end=[]) for t in range(5)}
     chains = Counter()
     for t in range(a.skip + a.steps):
@@ -89,6 +89,11 @@ def main():
                              start_p10=pct(es, 10), start_p50=pct(es, 50), start_p90=pct(es, 90),
                              start_max=int(es.max()), conc25=conc[0], conc50=conc[1], conc75=conc[2],
                              wconc25=wconc[0], wconc50=wconc[1], wconc75=wconc[2]))
+        wt = buf[64:64 + 2 * KWT].reshape(KWT, 2).astype(np.int64)
+        wu = wt[:, 0] > 0
+        if wu.any():
+            gaps.append(int((p0 - wt[wu, 1].max()) * 10))     # last k_logic wave end -> first k_post block start
+            lspan.append(int((wt[wu, 1].max() - wt[wu, 0].min()) * 10))
         spans.append(int(span))
         enc_ends.append(int(enc_end))
         last_item = int(np.argmax(en)) if n else -1
@@ -104,6 +109,8 @@ def main():
         buf[:] = 0
     out = dict(cfg=a.cfg, steps=a.steps, skip=a.skip, spawn_ahead=a.spawn_ahead,
                span_ns=dict(p50=pct(spans, 50), p90=pct(spans, 90), max=int(max(spans))),
+               k_logic_span_ns=dict(p50=pct(lspan, 50), p90=pct(lspan, 90)),
+               logic_end_to_post_start_ns=dict(p10=pct(gaps, 10), p50=pct(gaps, 50), p90=pct(gaps, 90)),
                enc_end_ns=dict(p50=pct(enc_ends, 50), p90=pct(enc_ends, 90)),
                last_to_end=dict(crit),
                encode_blocks={k: int(np.median([x[k] for x in encs])) for k in encs[0]} if encs else None,
