@@ -169,7 +169,8 @@ def main():
     ap.add_argument('--vision-range', type=int, default=None)
     ap.add_argument('--frame-stack', type=int, default=None)
     ap.add_argument('--spawn-background', type=int, default=0,
-                    help='snake_cfg.spawn_background: 0 automatic (boards over 8 192 spawn poses), 1 on, -1 off')
+                    help='snake_cfg.spawn_background: 0 automatic (boards over 8 192 spawn poses, batches '
+                         'of up to 8 192 envs and 64 MiB of observations), 1 on, -1 off')
     ap.add_argument('--spawn-ahead', type=int, default=0,
                     help='snake_cfg.spawn_ahead: 0 default threshold, -1 off, k: envs with at most k live snakes')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)

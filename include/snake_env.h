@@ -53,13 +53,14 @@ typedef struct {
                                    2 = reset every env after every step (gym 0.23.1's
                                    worker behind make_snake, wrappers.py:212) */
     int32_t spawn_ahead;        /* spawn-ahead threshold (snake_step): 0 = default (at most
-                                   2 live snakes, every env under coop), -1 = off, k >= 1 =
+                                   3 live snakes, every env under coop), -1 = off, k >= 1 =
                                    envs with at most k live snakes. Never changes results. */
     int32_t spawn_background;   /* 1 = the spawn-ahead attempts run in a background kernel on a
                                    stream of the library's that outlives snake_step (see
                                    snake_sync, snake_release), 0 = automatic (on for boards of
-                                   more than 8192 spawn poses, e.g. 40x40), -1 = off (inside the
-                                   step). Needs spawn-ahead on and a draw record that fits LDS
+                                   more than 8192 spawn poses, e.g. 40x40, and for batches of
+                                   at most 8192 envs and 64 MiB of observations per step),
+                                   -1 = off (inside the step). Needs spawn-ahead on and a draw record that fits LDS
                                    (at most 18 368 spawn poses). Never changes results. */
 } snake_cfg;
 

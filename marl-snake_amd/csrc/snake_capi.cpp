@@ -268,11 +268,21 @@ static int spawn_thr_of(const snake_cfg *c)
 // does, for the queue set). Needs spawn-ahead on (all-done auto-reset) and the
 // draw record in LDS. cfg->spawn_background: 0 automatic, 1 on, -1 off.
 // Automatic: boards of more than 8192 spawn poses, whose attempt outlasts a
-// step (40x40: ~110 us); at 20x20 the background jobs slowed the concurrent
-// encodes more than they saved (cfg3 0.111 -> 0.124 ms with the one-step wait).
-static bool bg_of(const snake_cfg *c, int64_t n_cand)
+// step (40x40: ~110 us), and small batches (<= 8192 envs, <= 64 MiB of
+// observations per step), whose step is otherwise one in-step attempt's latency.
+// Round 5 (one background stream per queue set, resets waiting for a record
+// being drawn), same-box medians in ms: cfg2 (4096 envs) 0.0435 -> 0.0412, 1024
+// envs 0.0404 -> 0.0340, cfg3 geometry at 8192 envs 0.0448 -> 0.0434; larger
+// batches lose, the jobs slowing the concurrent encodes more than they save:
+// cfg2 geometry at 8192 (100 MiB) 0.0460 -> 0.0512, cfg3 geometry at 16384
+// 0.0495 -> 0.0539, cfg4 0.0580 -> 0.0672, cfg3 0.0838 -> 0.0887.
+static bool bg_of(const snake_cfg *c, int64_t n_cand, int64_t N)
 {
-    const bool want = c->spawn_background != 0 ? c->spawn_background > 0 : n_cand > 8192;
+    const int64_t oh = c->vision_range ? 2 * c->vision_range + 1 : c->height;
+    const int64_t ow = c->vision_range ? 2 * c->vision_range + 1 : c->width;
+    const int64_t obs = N * c->num_snakes * oh * ow * 8 * c->frame_stack;
+    const bool small = N <= 8192 && obs <= ((int64_t)64 << 20);
+    const bool want = c->spawn_background != 0 ? c->spawn_background > 0 : (n_cand > 8192 || small);
     return want && spawn_thr_of(c) >= 0 && 2 * (n_cand + kWave) <= kJarrLdsMax;
 }
 
@@ -363,7 +373,7 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax && !lean_workers)
                       ? 0 : std::min<int64_t>(N, kResetSlots) * link;
     // (background spawn-ahead: two records per env, see k_spawn)
-    o->spawn = (bg_of(c, o->n_cand) ? 2 : 1) * N * kSpawnStride * 4;
+    o->spawn = (bg_of(c, o->n_cand, N) ? 2 : 1) * N * kSpawnStride * 4;
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
         // kQShards) with room for every env of its blocks, + the step's counters
         // (kQCount, each in its own line); sized for any k_logic lane grouping
@@ -460,13 +470,13 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // attempt) -- cfg2 0.0451 -> 0.0430 ms, cfg4 0.0627 -> 0.0602; at 65 536
     // envs the doubled LDS costs the encodes their occupancy (cfg3 0.0842 ->
     // 0.0994), so there the u16 record stays
-    if (k->link_in_lds && N <= 32768 && !bg_of(c, n_cand) && 4 * (int64_t)k->link_stride <= kJarrLdsMax) {
+    if (k->link_in_lds && N <= 32768 && !bg_of(c, n_cand, N) && 4 * (int64_t)k->link_stride <= kJarrLdsMax) {
         k->link32 = 1;
         jbytes = 4 * k->link_stride;
     }
     // reset workers (<= kResetSlots, the global link tables are sized for that)
     k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
-    const bool bg = bg_of(c, n_cand);
+    const bool bg = bg_of(c, n_cand, N);
     // spawn-ahead jobs at 1, below the encodes; small batches with in-step
     // spawn-ahead higher (a lone attempt is there the step's critical path:
     // cfg2 0.0510 -> 0.0494 ms; at cfg3 it costs 0.0905 -> 0.0960). Until round

@@ -6,6 +6,13 @@ lines it spans (from -gline-tables-only .loc directives). VERDICT r2 item 2:
 count the lane moves inside the draw-round and trace loops before changing them.
 
     python scripts/loop_spills.py [kernel-substring] [extra hipcc flags...]
+    python scripts/loop_spills.py --sites k1 k2 ...   (one summary line per kernel)
+
+--sites: every spill move (v_writelane into a spill VGPR, v_readlane from one)
+with the source line it belongs to (the last non-zero .loc) and the innermost
+loop around it (with that loop's source-line span): the moves on the per-job
+path versus those inside the draw-round / trace / encode loops (VERDICT r4
+item 6).
 """
 import json
 import os
@@ -27,15 +34,64 @@ def kernel_body(text, sub):
     sys.exit('kernel not found: ' + sub)
 
 
-def main():
-    sub = sys.argv[1] if len(sys.argv) > 1 else 'k_autoresetILi4ELb0ELb0E'
+def compile_asm(extra):
     with tempfile.TemporaryDirectory() as d:
         asm = os.path.join(d, 'k.s')
-        r = subprocess.run(['/opt/rocm/bin/hipcc'] + FLAGS + ['-S', SRC, '-o', asm] + sys.argv[2:],
+        r = subprocess.run(['/opt/rocm/bin/hipcc'] + FLAGS + ['-S', SRC, '-o', asm] + extra,
                            capture_output=True, text=True)
         if r.returncode:
             sys.exit(r.stderr[-2000:])
-        text = open(asm).read()
+        return open(asm).read()
+
+
+def sites(text, sub):
+    """Spill moves of one kernel by source line and innermost loop."""
+    name, lines = kernel_body(text, sub)
+    ins, labels, cur = [], {}, 0
+    for ln in lines:
+        s = ln.strip()
+        m = re.match(r'\.loc\s+\d+\s+(\d+)', s)
+        if m:
+            cur = int(m.group(1)) or cur   # (line 0: compiler-made code, keep the last line)
+            continue
+        m = re.match(r'^(\.LBB\w+):', s)
+        if m:
+            labels[m.group(1)] = len(ins)
+            continue
+        if ln.startswith('\t') and s and not s.startswith(('.', ';')):
+            ins.append((s, cur))
+    spill_v = {m.group(1) for s, _ in ins for m in [re.match(r'v_writelane_b32\s+(v\d+)', s)] if m}
+    loops = sorted({(labels[m.group(1)], j) for j, (s, _) in enumerate(ins)
+                    for m in [re.match(r's_(?:cbranch_\w+|branch)\s+(\.LBB\w+)', s)]
+                    if m and m.group(1) in labels and labels[m.group(1)] <= j})
+    by = {}
+    for j, (s, line) in enumerate(ins):
+        st = re.match(r'v_writelane_b32\s+(v\d+)', s)
+        ld = re.match(r'v_readlane_b32\s+\w+,\s*(v\d+)', s)
+        if not (st or (ld and ld.group(1) in spill_v)):
+            continue
+        inner = min((l for l in loops if l[0] <= j <= l[1]), key=lambda l: l[1] - l[0], default=None)
+        if inner:
+            src = [c for _, c in ins[inner[0]:inner[1] + 1] if c]
+            key = f'loop {min(src)}-{max(src)} ({inner[1] - inner[0] + 1} instructions)'
+        else:
+            key = 'straight-line'
+        d = by.setdefault(key, {'stores': 0, 'reloads': 0, 'lines': set()})
+        d['stores' if st else 'reloads'] += 1
+        d['lines'].add(line)
+    return {'kernel': name, 'instructions': len(ins), 'spill_vgprs': sorted(spill_v),
+            'sites': {k: {'stores': v['stores'], 'reloads': v['reloads'], 'src_lines': sorted(v['lines'])}
+                      for k, v in sorted(by.items())}}
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == '--sites':
+        text = compile_asm([])
+        for sub in sys.argv[2:]:
+            print(json.dumps(sites(text, sub)))
+        return
+    sub = sys.argv[1] if len(sys.argv) > 1 else 'k_autoresetILi4ELb0ELb0E'
+    text = compile_asm(sys.argv[2:])
     name, lines = kernel_body(text, sub)
     files = {m.group(1): m.group(2) for m in re.finditer(r'^\s*\.file\s+(\d+)\s+"[^"]*"\s+"([^"]+)"', text, re.M)}
     # instruction stream with the current source line

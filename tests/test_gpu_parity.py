@@ -265,8 +265,10 @@ def test_full_size_sampled_parity(oracle, case):
 
 
 @pytest.mark.parametrize('S,kw,spawn', [
-    # dict: the background spawn kernel (on by default only for boards of more than 8192 poses)
-    (4, dict(height=20, width=20, vision_range=5), (0, -1, 1, 4, dict(spawn_ahead=0, spawn_background=1))),
+    # dict: the background spawn kernel on / off (on by default for boards of
+    # more than 8192 poses and for batches of up to 8192 envs like this one)
+    (4, dict(height=20, width=20, vision_range=5),
+     (0, -1, 1, 4, dict(spawn_ahead=0, spawn_background=-1), dict(spawn_ahead=3, spawn_background=-1))),
     (4, dict(height=12, width=12, coop=True), (0, -1)),             # coop: every env queued
     # 40x40, two frames: four-wave lean encodes (k_post_lean). By default the
     # attempts run in the background kernel; spawn_background=-1 runs them in

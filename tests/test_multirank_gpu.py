@@ -38,12 +38,14 @@ def _run(cmd, tmp_path, name):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize('config,per', [('cfg3', 768), ('cfg5', 96)])
-def test_two_ranks_equal_one_process(tmp_path, config, per):
+@pytest.mark.parametrize('config,per,bg', [('cfg3', 768, -1), ('cfg3', 768, 0), ('cfg5', 96, 0)])
+def test_two_ranks_equal_one_process(tmp_path, config, per, bg):
+    """bg: --spawn-background (0 automatic: on for both of these small shards,
+    -1 the in-step spawn-ahead of large 20x20 shards)."""
     if not os.path.exists(os.path.join(ROOT, 'marl-snake_amd', 'marlenv', 'libsnake_amd.so')):
         pytest.fail('libsnake_amd.so not built')
     common = ['--steps', '40', '--warmup', '10', '--no-cpu-baseline', '--timing-stride', '4',
-              '--global-actions', '--config', config]
+              '--global-actions', '--config', config, '--spawn-background', str(bg)]
     two = tmp_path / 'two'
     lines = _run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
                   '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), 'bench.py', '--gpus', '2',
@@ -62,10 +64,10 @@ def test_two_ranks_equal_one_process(tmp_path, config, per):
     assert [(int(p['lo']), int(p['hi'])) for p in parts] == [(0, per), (per, 2 * per)]
     for key in ('grids', 'mt', 'mt_pos', 'env', 'obs', 'rew_sum'):
         cat, ref = np.concatenate([p[key] for p in parts]), full[key]
-        if key == 'env' and config == 'cfg5':
-            # background spawn-ahead (40x40): the status word (ENV_SPAWN, word 4:
-            # record status + generation) depends on when each k_spawn finished
-            # relative to the steps -- bookkeeping, not env state
+        if key == 'env' and bg >= 0:
+            # background spawn-ahead: the status word (ENV_SPAWN, word 4: record
+            # status + generation) depends on when each k_spawn finished relative
+            # to the steps -- bookkeeping, not env state
             cat, ref = np.delete(cat, 4, axis=1), np.delete(ref, 4, axis=1)
         assert cat.tobytes() == ref.tobytes(), key
     if config == 'cfg3':   # the rollout went through episode ends (auto-resets on both ranks)
@@ -78,7 +80,8 @@ def test_rccl_rank_equals_plain_process(tmp_path):
     on the box's GPU, the same rollout as the plain process, one JSON line whose
     time went through the device-side all_reduce(MAX)."""
     common = ['--steps', '30', '--warmup', '10', '--no-cpu-baseline', '--timing-stride', '4',
-              '--global-actions', '--config', 'cfg3', '--envs-per-gpu', '1024']
+              '--global-actions', '--config', 'cfg3', '--envs-per-gpu', '1024',
+              '--spawn-background', '-1']   # (in-step spawn-ahead: the status word is exact too)
     r = tmp_path / 'rccl'
     lines = _run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
                   '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), 'bench.py', '--gpus', '1',
