@@ -17,6 +17,7 @@
 // Compiled with -ffp-contract=off: rewards/statistics are float64 in the
 // reference's order of operations (snake_env.py:365-369, :385-389).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <limits.h>
 #include <stdlib.h>
@@ -34,6 +35,20 @@
 constexpr int kResetWavesPerEU = 4;   // reset workers: 128 VGPRs (3 waves/SIMD measured slower)
 
 namespace snake {
+
+// Every launch goes through hipExtLaunchKernel: while a launch is timed
+// (TimedLaunch, snake_timing_enable) these are its start/stop events, which then
+// carry the dispatch's own begin/end timestamps -- no marker packets of their
+// own between the step's kernels (hipEventRecord pairs left 6 + 10.5 us gaps
+// around each timed step's k_logic / k_post in the kernel trace). Null: a
+// plain launch.
+thread_local hipEvent_t t_ev0 = nullptr, t_ev1 = nullptr;
+template <typename F, typename... Args>
+static inline void slaunch(F kernel, const dim3 &grid, const dim3 &block, uint32_t lds, hipStream_t s,
+                           Args... args)
+{
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, s, t_ev0, t_ev1, 0u, args...);
+}
 
 __device__ unsigned long long g_resets_run;     // auto-resets run (snake_timing_read "resets")
 __device__ unsigned long long g_resets_timed;   // the same, while timing is enabled ("resets_timed")
@@ -2816,39 +2831,47 @@ hipEvent_t pooled_event()
         return ev;
     }
     hipEvent_t ev = nullptr;
-    // device-scope release: a timing event need not write the L2 back for the host
-    if (hipEventCreateWithFlags(&ev, hipEventReleaseToDevice) != hipSuccess) return nullptr;
+    // timing only: no system-scope fence (cache write-back and invalidate) when
+    // the event completes, which would delay the next kernel
+    if (hipEventCreateWithFlags(&ev, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     return ev;
 }
 }  // namespace
 
-// Brackets one launch: open() before it, close() after it (no-ops when off).
+// Times the one launch (slaunch) made between its construction and close():
+// the pair of pooled events rides on that launch (no-ops when timing is off).
 struct TimedLaunch {
     const char *name;
-    hipStream_t s;
-    hipEvent_t a = nullptr;
-    TimedLaunch(const char *n, hipStream_t st) : name(n), s(st)
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedLaunch(const char *n, hipStream_t) : name(n)
     {
         std::lock_guard<std::mutex> g(g_tmu);
         if (!g_timing) return;
         a = pooled_event();
-        if (a && hipEventRecord(a, s) != hipSuccess) {
-            g_pool.push_back(a);
+        b = a ? pooled_event() : nullptr;
+        if (!b) {
+            if (a) g_pool.push_back(a);
             a = nullptr;
+            return;
         }
+        t_ev0 = a;
+        t_ev1 = b;
     }
     void close()
     {
         if (!a) return;
+        t_ev0 = t_ev1 = nullptr;
         std::lock_guard<std::mutex> g(g_tmu);
-        hipEvent_t b = pooled_event();
-        if (b && hipEventRecord(b, s) == hipSuccess) {
-            g_pending.push_back({name, a, b});
-        } else {
+        // (a failed launch records neither: check_launch reports it, the pair
+        // goes back to the pool)
+        if (hipPeekAtLastError() == hipSuccess) g_pending.push_back({name, a, b});
+        else {
             g_pool.push_back(a);
-            if (b) g_pool.push_back(b);
+            g_pool.push_back(b);
         }
+        a = nullptr;
     }
+    ~TimedLaunch() { close(); }
 };
 
 // Every launch runs with the caller stream's device current: the side stream and
@@ -2980,7 +3003,7 @@ int launch_seed(const KCfg &k, const snake_state &st, uint32_t base_seed, int64_
     DeviceGuard dg((hipStream_t)stream);
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
     if (int rc = wait_background(st, stream)) return rc;
-    hipLaunchKernelGGL(k_seed, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, k, st,
+    slaunch(k_seed, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, k, st,
                        base_seed, (long long)env_offset);
     return check_launch("k_seed");
 }
@@ -2995,7 +3018,7 @@ int launch_render(const KCfg &k, const snake_state &st, const uint8_t *palette, 
     const long long quads = ((long long)k.N * k.HW + 3) / 4;
     const int threads = 256;
     const long long blocks = (quads + threads - 1) / threads;
-    hipLaunchKernelGGL(k_render, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream, k, st,
+    slaunch(k_render, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream, k, st,
                        pal, rgb);
     return check_launch("k_render");
 }
@@ -3011,17 +3034,17 @@ int launch_reset(const KCfg &k, const snake_state &st, const uint8_t *mask, cons
     const KArgs a{k, st, o, mask};
     const hipStream_t s = (hipStream_t)stream;
     if (k.link32) {
-        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, 2>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, 2>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_reset<16, 2>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) slaunch((k_reset<4, 2>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) slaunch((k_reset<8, 2>), grid, block, k.lds_bytes, s, a);
+        else slaunch((k_reset<16, 2>), grid, block, k.lds_bytes, s, a);
     } else if (k.link_in_lds) {
-        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, 1>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, 1>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_reset<16, 1>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) slaunch((k_reset<4, 1>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) slaunch((k_reset<8, 1>), grid, block, k.lds_bytes, s, a);
+        else slaunch((k_reset<16, 1>), grid, block, k.lds_bytes, s, a);
     } else {
-        if (k.S <= 4) hipLaunchKernelGGL((k_reset<4, 0>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_reset<8, 0>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_reset<16, 0>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) slaunch((k_reset<4, 0>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) slaunch((k_reset<8, 0>), grid, block, k.lds_bytes, s, a);
+        else slaunch((k_reset<16, 0>), grid, block, k.lds_bytes, s, a);
     }
     tl.close();
     return check_launch("k_reset");
@@ -3032,12 +3055,12 @@ template <int MS, bool RO, int JL>
 static void launch_post(const KCfg &k, const KArgs &a, int npf, dim3 grid, int lds, hipStream_t s)
 {
     const dim3 block(kWave);
-    if (npf == 0) hipLaunchKernelGGL((k_post<MS, 0, RO, JL>), grid, block, lds, s, a);
-    else if (npf == -2) hipLaunchKernelGGL((k_post<MS, -2, RO, JL>), grid, block, lds, s, a);
-    else if (npf == -8) hipLaunchKernelGGL((k_post<MS, -8, RO, JL>), grid, block, lds, s, a);
-    else if (npf == 1) hipLaunchKernelGGL((k_post<MS, 1, RO, JL>), grid, block, lds, s, a);
-    else if (npf == 2) hipLaunchKernelGGL((k_post<MS, 2, RO, JL>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((k_post<MS, 8, RO, JL>), grid, block, lds, s, a);
+    if (npf == 0) slaunch((k_post<MS, 0, RO, JL>), grid, block, lds, s, a);
+    else if (npf == -2) slaunch((k_post<MS, -2, RO, JL>), grid, block, lds, s, a);
+    else if (npf == -8) slaunch((k_post<MS, -8, RO, JL>), grid, block, lds, s, a);
+    else if (npf == 1) slaunch((k_post<MS, 1, RO, JL>), grid, block, lds, s, a);
+    else if (npf == 2) slaunch((k_post<MS, 2, RO, JL>), grid, block, lds, s, a);
+    else slaunch((k_post<MS, 8, RO, JL>), grid, block, lds, s, a);
 }
 
 template <bool RO, int JL>
@@ -3053,13 +3076,13 @@ static void launch_autoreset_ro(const KCfg &k, const KArgs &a, dim3 grid, hipStr
 {
     const dim3 block(kWave);
     if (k.link_in_lds) {
-        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true, 1>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true, 1>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_autoreset<16, true, 1>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) slaunch((k_autoreset<4, true, 1>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) slaunch((k_autoreset<8, true, 1>), grid, block, k.lds_bytes, s, a);
+        else slaunch((k_autoreset<16, true, 1>), grid, block, k.lds_bytes, s, a);
     } else {
-        if (k.S <= 4) hipLaunchKernelGGL((k_autoreset<4, true, 0>), grid, block, k.lds_bytes, s, a);
-        else if (k.S <= 8) hipLaunchKernelGGL((k_autoreset<8, true, 0>), grid, block, k.lds_bytes, s, a);
-        else hipLaunchKernelGGL((k_autoreset<16, true, 0>), grid, block, k.lds_bytes, s, a);
+        if (k.S <= 4) slaunch((k_autoreset<4, true, 0>), grid, block, k.lds_bytes, s, a);
+        else if (k.S <= 8) slaunch((k_autoreset<8, true, 0>), grid, block, k.lds_bytes, s, a);
+        else slaunch((k_autoreset<16, true, 0>), grid, block, k.lds_bytes, s, a);
     }
 }
 
@@ -3096,13 +3119,13 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         constexpr int WPB = decltype(wpb)::value;
         const dim3 glb((gl.x + WPB - 1) / WPB), blb(kWave * WPB);
         if (k.bg) {
-            if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
-            else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
-            else hipLaunchKernelGGL((k_logic<16, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+            if (ms == 4) slaunch((k_logic<4, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+            else if (ms == 8) slaunch((k_logic<8, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
+            else slaunch((k_logic<16, WPB, true>), glb, blb, WPB * lds_logic, sm, la);
         } else {
-            if (ms == 4) hipLaunchKernelGGL((k_logic<4, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
-            else if (ms == 8) hipLaunchKernelGGL((k_logic<8, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
-            else hipLaunchKernelGGL((k_logic<16, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+            if (ms == 4) slaunch((k_logic<4, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+            else if (ms == 8) slaunch((k_logic<8, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
+            else slaunch((k_logic<16, WPB, false>), glb, blb, WPB * lds_logic, sm, la);
         }
     };
     if (k.logic_wpb == 4) launch_logic(std::integral_constant<int, 4>{});
@@ -3135,13 +3158,13 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         t2.close();
         if ((rc = check_launch("k_autoreset"))) return fail(rc);
         TimedLaunch t3("k_encode", sm);
-        hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
+        slaunch(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
         t3.close();
         return check_launch("k_encode");
     }
     if (!k.autoreset) {
         TimedLaunch t3("k_encode", sm);
-        hipLaunchKernelGGL(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
+        slaunch(k_encode, g1, block, k.lds_obs_bytes, sm, k, st, o);
         t3.close();
         return check_launch("k_encode");
     }
@@ -3159,9 +3182,9 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         const dim3 gs(k.spawn_slots);
         TimedLaunch t4("k_spawn", bx);
         const KArgs sa{ks, st, o, nullptr};
-        if (k.S <= 4) hipLaunchKernelGGL(k_spawn<4>, gs, block, lds_sp, bx, sa);
-        else if (k.S <= 8) hipLaunchKernelGGL(k_spawn<8>, gs, block, lds_sp, bx, sa);
-        else hipLaunchKernelGGL(k_spawn<16>, gs, block, lds_sp, bx, sa);
+        if (k.S <= 4) slaunch(k_spawn<4>, gs, block, lds_sp, bx, sa);
+        else if (k.S <= 8) slaunch(k_spawn<8>, gs, block, lds_sp, bx, sa);
+        else slaunch(k_spawn<16>, gs, block, lds_sp, bx, sa);
         t4.close();
         if ((rc = check_launch("k_spawn"))) return fail(rc);
         // (counted as soon as it is launched: its last worker adds one to the
@@ -3182,22 +3205,22 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         const int lds_p = std::max(4 * k.lds_worker, k.tbl ? k.lds_tbl_bytes : k.lds_lean_bytes);
         if (k.tbl) {   // (the table encode in four-wave workgroups)
             if (k.bg) {
-                if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, true, true>), gp, dim3(256), lds_p, sm, a);
-                else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, true, true>), gp, dim3(256), lds_p, sm, a);
-                else hipLaunchKernelGGL((k_post_lean<16, true, true>), gp, dim3(256), lds_p, sm, a);
+                if (k.S <= 4) slaunch((k_post_lean<4, true, true>), gp, dim3(256), lds_p, sm, a);
+                else if (k.S <= 8) slaunch((k_post_lean<8, true, true>), gp, dim3(256), lds_p, sm, a);
+                else slaunch((k_post_lean<16, true, true>), gp, dim3(256), lds_p, sm, a);
             } else {
-                if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, false, true>), gp, dim3(256), lds_p, sm, a);
-                else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, false, true>), gp, dim3(256), lds_p, sm, a);
-                else hipLaunchKernelGGL((k_post_lean<16, false, true>), gp, dim3(256), lds_p, sm, a);
+                if (k.S <= 4) slaunch((k_post_lean<4, false, true>), gp, dim3(256), lds_p, sm, a);
+                else if (k.S <= 8) slaunch((k_post_lean<8, false, true>), gp, dim3(256), lds_p, sm, a);
+                else slaunch((k_post_lean<16, false, true>), gp, dim3(256), lds_p, sm, a);
             }
         } else if (k.bg) {
-            if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, true, false>), gp, dim3(256), lds_p, sm, a);
-            else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, true, false>), gp, dim3(256), lds_p, sm, a);
-            else hipLaunchKernelGGL((k_post_lean<16, true, false>), gp, dim3(256), lds_p, sm, a);
+            if (k.S <= 4) slaunch((k_post_lean<4, true, false>), gp, dim3(256), lds_p, sm, a);
+            else if (k.S <= 8) slaunch((k_post_lean<8, true, false>), gp, dim3(256), lds_p, sm, a);
+            else slaunch((k_post_lean<16, true, false>), gp, dim3(256), lds_p, sm, a);
         } else {
-            if (k.S <= 4) hipLaunchKernelGGL((k_post_lean<4, false, false>), gp, dim3(256), lds_p, sm, a);
-            else if (k.S <= 8) hipLaunchKernelGGL((k_post_lean<8, false, false>), gp, dim3(256), lds_p, sm, a);
-            else hipLaunchKernelGGL((k_post_lean<16, false, false>), gp, dim3(256), lds_p, sm, a);
+            if (k.S <= 4) slaunch((k_post_lean<4, false, false>), gp, dim3(256), lds_p, sm, a);
+            else if (k.S <= 8) slaunch((k_post_lean<8, false, false>), gp, dim3(256), lds_p, sm, a);
+            else slaunch((k_post_lean<16, false, false>), gp, dim3(256), lds_p, sm, a);
         }
     } else {
         // the workers, then the encodes: NPF = 16-byte ring chunks per lane the
@@ -3324,7 +3347,7 @@ __global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsi
 // out_dev: [draw cycles, final MT position, trace cycles, arr[0]]
 extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, int S, unsigned long long *out_dev)
 {
-    hipLaunchKernelGGL(k_drawbench, dim3(1), dim3(64), 2 * n + 256, 0, mt_dev, pos0, n, S, out_dev);
+    slaunch(k_drawbench, dim3(1), dim3(64), 2 * n + 256, 0, mt_dev, pos0, n, S, out_dev);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
@@ -3391,13 +3414,13 @@ extern "C" int snake_debug_attemptbench(const uint32_t *mt_dev, int pos0, int n,
     const int lds = 256 + (jl == 1 ? 2 * (n + kWave) : (jl == 2 ? 4 * stride : 0));
     const dim3 g(1), b(coop ? kWave * kCoopW : kWave);
     if (coop) {
-        if (jl == 1) hipLaunchKernelGGL((k_attemptbench<true, 1>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-        else if (jl == 2) hipLaunchKernelGGL((k_attemptbench<true, 2>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-        else hipLaunchKernelGGL((k_attemptbench<true, 0>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        if (jl == 1) slaunch((k_attemptbench<true, 1>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        else if (jl == 2) slaunch((k_attemptbench<true, 2>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        else slaunch((k_attemptbench<true, 0>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
     } else {
-        if (jl == 1) hipLaunchKernelGGL((k_attemptbench<false, 1>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-        else if (jl == 2) hipLaunchKernelGGL((k_attemptbench<false, 2>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-        else hipLaunchKernelGGL((k_attemptbench<false, 0>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        if (jl == 1) slaunch((k_attemptbench<false, 1>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        else if (jl == 2) slaunch((k_attemptbench<false, 2>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
+        else slaunch((k_attemptbench<false, 0>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
     }
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
