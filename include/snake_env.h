@@ -53,7 +53,8 @@ typedef struct {
                                    2 = reset every env after every step (gym 0.23.1's
                                    worker behind make_snake, wrappers.py:212) */
     int32_t spawn_ahead;        /* spawn-ahead threshold (snake_step): 0 = default (at most
-                                   3 live snakes, every env under coop), -1 = off, k >= 1 =
+                                   3 live snakes, 4 on small background batches of at most
+                                   8192 spawn poses, every env under coop), -1 = off, k >= 1 =
                                    envs with at most k live snakes. Never changes results. */
     int32_t spawn_background;   /* 1 = the spawn-ahead attempts run in a background kernel on a
                                    stream of the library's that outlives snake_step (see

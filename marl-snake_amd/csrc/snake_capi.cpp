@@ -517,6 +517,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     k->q_envs_per_block = kWave / k->logic_ms;
     k->q_cap = (int)queue_cap(N, k->q_envs_per_block);
     k->spawn_thr = spawn_thr_of(c);
+    // small batches with the background kernel: the attempts leave the step and
+    // the CUs have room, so one live snake more (round 5, same box, ms per step,
+    // threshold 3 -> 4: cfg2 0.0409 -> 0.0403, cfg3 geometry at 8 192 envs
+    // 0.0434 -> 0.0425; 40x40 boards unchanged at 3: cfg5 0.0826 vs 0.0827)
+    if (bg && c->spawn_ahead == 0 && !c->coop && n_cand <= 8192 && k->spawn_thr == 3) k->spawn_thr = 4;
     k->bg = bg ? 1 : 0;
     k->spawn_slots = (int)std::min<int64_t>(N, kResetSlots);   // k_spawn workers
     k->bg_tries = 1;   // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
