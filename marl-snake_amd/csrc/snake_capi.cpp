@@ -477,6 +477,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // reset workers (<= kResetSlots, the global link tables are sized for that)
     k->reset_slots = (int)std::min<int64_t>(N, kResetSlots);
     const bool bg = bg_of(c, n_cand, N);
+    // small boards with the background kernel: the workers only paint resets
+    // from records (≈65 per step at cfg2), so 512 of them (same box, ms per
+    // step: cfg2 0.0399 -> 0.0394 and 0.0401 -> 0.0397; 256: 0.0397; 40x40
+    // boards within noise at 256-1024, kept at 2 048)
+    if (bg && n_cand <= 8192) k->reset_slots = (int)std::min<int64_t>(N, 512);
     // spawn-ahead jobs at 1, below the encodes; small batches with in-step
     // spawn-ahead higher (a lone attempt is there the step's critical path:
     // cfg2 0.0510 -> 0.0494 ms; at cfg3 it costs 0.0905 -> 0.0960). Until round
@@ -488,14 +493,16 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // 0.1275 -> 0.1200 ms against the hardware default 0). With background
     // spawn-ahead the step's resets are the critical path beside the encodes
     // instead: 0 (cfg5 0.160 -> 0.135 ms).
-    k->encode_prio = bg ? 0 : 2;
+    k->encode_prio = bg ? 0 : 2;   // (2 on small background boards: cfg2 0.0399 -> 0.0403)
+
     {
         // k_logic's lanes per env (4, 8 or 16 >= S; 64 / that = envs per wave):
         // the fewest lanes that hold S snakes; small batches at least 8 (more,
         // shorter waves: cfg2's 4 096 envs k_logic 16.4 -> 15.3 us, step 0.0540
         // -> 0.0527 ms; 16 lanes 18.0 us; at cfg3 8 lanes cost 6 us)
         const int ms_min = k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16);
-        k->logic_ms = N <= 8192 ? std::max(ms_min, 8) : ms_min;
+        k->logic_ms = N <= 8192 ? std::max(ms_min, 8) : ms_min;   // (round 5, background cfg2: 4 lanes 0.0403 vs 0.0399)
+
     }
     // k_logic's LDS carve (snake_kernels.hip k_logic) per wave: E frames, the
     // fruit buffer, the respawn raws and cells
