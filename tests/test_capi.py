@@ -80,6 +80,24 @@ def test_plan_sizes(native):
     assert lay.jscratch == 64 * (16424 + 64) * 4 and lay.spawn == 64 * 672 * 4
 
 
+@pytest.mark.parametrize('kw,N,bg', [
+    (dict(height=20, width=20), 4096, True),                     # cfg2: 50 MiB of obs per step
+    (dict(height=20, width=20), 8192, False),                    # 100 MiB
+    (dict(height=20, width=20, vision_range=5), 8192, True),     # cfg3's board at 8 192 envs
+    (dict(height=20, width=20, vision_range=5), 16384, False),   # more than 8 192 envs
+    (dict(height=20, width=20, spawn_background=-1), 4096, False),
+    (dict(height=20, width=20, spawn_ahead=-1), 1024, False),    # nothing to draw ahead
+])
+def test_plan_background_automatic(native, kw, N, bg):
+    """spawn_background = 0 (automatic) turns the background spawn kernel on for
+    batches of at most 8 192 envs and 64 MiB of observations per step (round 5):
+    the layout then holds two spawn-ahead records per env."""
+    c = cfg(native, num_snakes=4, **kw)
+    lay = native.SnakeLayout()
+    assert native.lib().snake_plan(ctypes.byref(c), N, ctypes.byref(lay)) == 0
+    assert lay.spawn == (2 if bg else 1) * N * 672 * 4, (kw, N)
+
+
 @pytest.mark.parametrize('H,W,L,N', [(50, 50, 3, 16384), (72, 72, 3, 4096), (100, 100, 2, 65536)])
 def test_plan_large_boards(native, H, W, L, N):
     """Boards whose k_logic frames do not fit four waves per workgroup (ADVICE r4:
