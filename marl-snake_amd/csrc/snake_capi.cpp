@@ -530,7 +530,10 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // 0.0434 -> 0.0425; 40x40 boards unchanged at 3: cfg5 0.0826 vs 0.0827)
     if (bg && c->spawn_ahead == 0 && !c->coop && n_cand <= 8192 && k->spawn_thr == 3) k->spawn_thr = 4;
     k->bg = bg ? 1 : 0;
-    k->spawn_slots = (int)std::min<int64_t>(N, kResetSlots);   // k_spawn workers
+    // k_spawn workers: 512 on small background boards (≈130 jobs per step at
+    // cfg2: 0.0397 -> 0.0391 ms, same box; 256: 0.0392), 2 048 on 40x40 (cfg5:
+    // 512 0.0827-0.0832, 1 024 0.0822, 2 048 0.0823)
+    k->spawn_slots = (int)std::min<int64_t>(N, bg && n_cand <= 8192 ? 512 : kResetSlots);
     k->bg_tries = 1;   // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
     k->spawn_tries = 1;   // attempts per in-step spawn-ahead job (2 measured cfg3 0.0875 -> 0.103 ms: a retry doubles the chain)
     k->lds_obs_bytes = off;
