@@ -184,6 +184,8 @@ def main():
     ap.add_argument('--dump-dir', default=None,
                     help='write rank<r>.npz with the shard range, final grids, MT keys/positions, '
                          'env records, the last step\'s obs and each env\'s summed rewards')
+    ap.add_argument('--timing-warm', type=int, default=4,
+                    help='time (and drop) the last k warmup steps so the event pool is filled before the timed region')
     ap.add_argument('--timing-stride', type=int, default=None,
                     help='bracket the kernels of every k-th timed step with timing events '
                          '(0: none; default max(1, min(32, steps // 4)), so at least 4 launches are '
@@ -250,15 +252,23 @@ def main():
     # outputs while the next step runs makes the allocator alternate between two
     # observation buffers; measured +4 us per step at cfg3)
     out = None
+    L = _native.lib()
     for t in range(args.warmup):
+        # the last --timing-warm warmup steps are timed and their timings dropped:
+        # the library's event pool then holds the events the timed steps use
+        # (creating them inside the timed region stalls the first timed steps)
+        warm = t >= args.warmup - args.timing_warm
+        if warm:
+            _native.timing_enable(True, L)
         if rsum is None:
             venv.step(actions[t])
         else:
             out = venv.step(actions[t])
             rsum += out[1]
+        if warm:
+            _native.timing_enable(False, L)
     torch.cuda.synchronize(device)
 
-    L = _native.lib()
     for k in ('k_logic', 'k_autoreset', 'k_encode', 'k_post', 'k_spawn', 'resets', 'resets_timed', 'spawn_hits',
               'spawn_jobs', 'spawn_void', 'reset_partial'):
         _native.timing_read(k, L)                      # drop anything from the warmup
