@@ -57,7 +57,7 @@ typedef struct {
                                    8192 spawn poses, every env under coop), -1 = off, k >= 1 =
                                    envs with at most k live snakes. Never changes results. */
     int32_t spawn_background;   /* 1 = the spawn-ahead attempts run in a background kernel on a
-                                   stream of the library's that outlives snake_step (see
+                                   stream of the library's (one per queue set) that outlives snake_step (see
                                    snake_sync, snake_release), 0 = automatic (on for boards of
                                    more than 8192 spawn poses, e.g. 40x40, and for batches of
                                    at most 8192 envs and 64 MiB of observations per step),

@@ -495,7 +495,7 @@ class SnakeVecEnv:
     def close(self):
         # the state buffers go back to the allocator on the current stream: order
         # that after a background spawn kernel still writing them, then release
-        # the library's background stream and events for this state (snake_release)
+        # the library's background streams and events for this state (snake_release)
         if getattr(self, '_state', None) is not None and torch_cuda_alive():
             try:
                 self.sync()
