@@ -2126,8 +2126,18 @@ __device__ void do_spawn(const KCfg &c, const snake_state &st, int e, uint8_t *l
 // auto-reset's claim (atomic add before it) -- so a job that sees another
 // generation has nothing to do, and one whose inputs were being rewritten fails
 // its final compare-and-swap (or is voided by the exchange landing after it).
-// The record goes to the buffer the status word does not point at: a reset that
-// claims the env meanwhile reads the other one, which nothing writes.
+// The record goes to buffer c.qpar, the job's queue set. Since round 5 the two
+// sets' kernels run on two streams and may overlap: a job voided by k_logic's
+// fruit draw (its word overwritten) may still be running when the next step's
+// k_logic queues the env again into the other set, whose job then draws from
+// the new state. Writing "the buffer the word does not point at" (as until
+// round 5) let both jobs write the same buffer -- k_logic's exchange clears the
+// buffer bit -- and a late write of the voided job could land in the published
+// record. With one buffer per set the two write different buffers; jobs of one
+// set run in order on one stream. A reset reads the buffer the word points at,
+// and the job that published it has finished; a job continuing a partial
+// record of its own set's buffer reads it whole (into registers) before it
+// overwrites it.
 template <int MS>
 __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_t qgen, uint8_t *lds, int lane)
 {
@@ -2162,7 +2172,7 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
         if (a > 0) wave_sync();
         ok = spawn_attempt<MS, 1>(c, st, mt, lds, 0, q, cell, lane);
     }
-    store_spawn_record<true>(c, st, e, mt, ok, cell, lane, spw, buf ^ 1);
+    store_spawn_record<true>(c, st, e, mt, ok, cell, lane, spw, c.qpar);
 }
 
 // Spawn-ahead right after an explicit reset (k_reset): the next episode's spawn
