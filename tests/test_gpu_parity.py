@@ -739,6 +739,43 @@ def test_background_state_lifetime():
     twin.close()
 
 
+@pytest.mark.parametrize('kw', [
+    dict(height=40, width=40, vision_range=5, num_fruits=24),   # 40x40: 110 us jobs, overlapping sets
+    dict(height=20, width=20, num_fruits=12),                   # small board, short jobs
+])
+def test_background_overlap_stress(kw):
+    """The background protocol under load (round 5: the two queue sets' spawn
+    kernels on two streams may overlap): many fruits, so k_logic's fruit draws
+    void records while their jobs still run and the env is queued again into
+    the other set; threshold 8 queues every env every step. The rollout must
+    equal the in-step spawn-ahead run bit for bit, step by step, and the env
+    state at the end."""
+    from marlenv import SnakeVecEnv, _native
+    N, S = 384, 8
+    bg = SnakeVecEnv(N, num_snakes=S, seed=21, spawn_ahead=8, spawn_background=1, **kw)
+    ref = SnakeVecEnv(N, num_snakes=S, seed=21, spawn_ahead=-1, spawn_background=-1, **kw)
+    assert torch.equal(bg.reset(), ref.reset())
+    g = torch.Generator(device='cuda').manual_seed(8)
+    for k in ('spawn_hits', 'spawn_void'):
+        _native.timing_read(k)
+    _native.timing_enable(True)
+    for t in range(200):
+        a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+        ob, rb, db, ib = bg.step(a)
+        orf, rr, dr, ir = ref.step(a)
+        assert torch.equal(ob, orf) and torch.equal(rb, rr) and torch.equal(db, dr), f'step {t}'
+        assert torch.equal(ib['episode_done'], ir['episode_done']), f'step {t}'
+    _native.timing_enable(False)
+    hits, voids = _native.timing_read('spawn_hits')[1], _native.timing_read('spawn_void')[1]
+    bg.sync()
+    assert torch.equal(bg.grids(), ref.grids()) and torch.equal(bg.mt, ref.mt)
+    er_b, er_r = bg.env_rec.view(N, 8), ref.env_rec.view(N, 8)
+    assert torch.equal(er_b[:, :4], er_r[:, :4])   # (word 4, the spawn-ahead status, is mode bookkeeping)
+    assert hits > 0 and voids > 0, (hits, voids)
+    bg.close()
+    ref.close()
+
+
 def test_info_read_on_another_stream():
     """The episode summary is filled on the stream the step ran on; read from
     another stream it is ordered after that fill: the values equal
