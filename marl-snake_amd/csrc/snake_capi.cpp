@@ -481,7 +481,8 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // from records (≈65 per step at cfg2), so 512 of them (same box, ms per
     // step: cfg2 0.0399 -> 0.0394 and 0.0401 -> 0.0397; 256: 0.0397; 40x40
     // boards within noise at 256-1024, kept at 2 048)
-    if (bg && n_cand <= 8192) k->reset_slots = (int)std::min<int64_t>(N, 512);
+    const bool bg_small = bg && n_cand <= 8192 && N <= 8192;   // (not a forced background kernel on a big batch)
+    if (bg_small) k->reset_slots = (int)std::min<int64_t>(N, 512);
     // spawn-ahead jobs at 1, below the encodes; small batches with in-step
     // spawn-ahead higher (a lone attempt is there the step's critical path:
     // cfg2 0.0510 -> 0.0494 ms; at cfg3 it costs 0.0905 -> 0.0960). Until round
@@ -494,7 +495,6 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // spawn-ahead the step's resets are the critical path beside the encodes
     // instead: 0 (cfg5 0.160 -> 0.135 ms).
     k->encode_prio = bg ? 0 : 2;   // (2 on small background boards: cfg2 0.0399 -> 0.0403)
-
     {
         // k_logic's lanes per env (4, 8 or 16 >= S; 64 / that = envs per wave):
         // the fewest lanes that hold S snakes; small batches at least 8 (more,
@@ -502,7 +502,6 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
         // -> 0.0527 ms; 16 lanes 18.0 us; at cfg3 8 lanes cost 6 us)
         const int ms_min = k->S <= 4 ? 4 : (k->S <= 8 ? 8 : 16);
         k->logic_ms = N <= 8192 ? std::max(ms_min, 8) : ms_min;   // (round 5, background cfg2: 4 lanes 0.0403 vs 0.0399)
-
     }
     // k_logic's LDS carve (snake_kernels.hip k_logic) per wave: E frames, the
     // fruit buffer, the respawn raws and cells
@@ -528,12 +527,12 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // the CUs have room, so one live snake more (round 5, same box, ms per step,
     // threshold 3 -> 4: cfg2 0.0409 -> 0.0403, cfg3 geometry at 8 192 envs
     // 0.0434 -> 0.0425; 40x40 boards unchanged at 3: cfg5 0.0826 vs 0.0827)
-    if (bg && c->spawn_ahead == 0 && !c->coop && n_cand <= 8192 && k->spawn_thr == 3) k->spawn_thr = 4;
+    if (bg_small && c->spawn_ahead == 0 && !c->coop && k->spawn_thr == 3) k->spawn_thr = 4;
     k->bg = bg ? 1 : 0;
     // k_spawn workers: 512 on small background boards (≈130 jobs per step at
     // cfg2: 0.0397 -> 0.0391 ms, same box; 256: 0.0392), 2 048 on 40x40 (cfg5:
     // 512 0.0827-0.0832, 1 024 0.0822, 2 048 0.0823)
-    k->spawn_slots = (int)std::min<int64_t>(N, bg && n_cand <= 8192 ? 512 : kResetSlots);
+    k->spawn_slots = (int)std::min<int64_t>(N, bg_small ? 512 : kResetSlots);
     k->bg_tries = 1;   // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
     k->spawn_tries = 1;   // attempts per in-step spawn-ahead job (2 measured cfg3 0.0875 -> 0.103 ms: a retry doubles the chain)
     k->lds_obs_bytes = off;
