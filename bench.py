@@ -1,20 +1,31 @@
 #!/usr/bin/env python3
 """Throughput of the batched multi-snake env step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg3s8|cfg4|cfg5]
+                    [--scaling strong|weak]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Workload (BASELINE.json metric, config 3 by default): 65 536 envs per GPU of
-20x20 grids, 4 snakes, vision_range=5, frame_stack=1, snake_length=3, default
+--gpus N > 1 without a launcher (no WORLD_SIZE in the environment) starts the N
+ranks itself: `python -m torch.distributed.run --nproc-per-node N` on this same
+command line, as a child process started before anything touches the GPU; rank
+0's JSON line is relayed (the children share stdout) and so is the return code.
+
+Workload (BASELINE.json metric, config 3 by default): 65 536 envs of 20x20
+grids, 4 snakes, vision_range=5, frame_stack=1, snake_length=3, default
 rewards, uniform random actions in {0,1,2} drawn up front on the device (seed
 12345), all-done auto-reset inside the step. Env i is seeded with its GLOBAL
-index, so ranks hold disjoint shards of one big batch (weak scaling, no
-collective on the step path; the only collectives are the timing barrier and
-max-reduce). --config picks BASELINE.json's other configs:
-  cfg2  4 096 envs/GPU, 20x20, 4 snakes, full-map observation
-  cfg3  65 536 envs/GPU, 20x20, 4 snakes, vision_range 5 (default)
-  cfg4  32 768 envs/GPU (262 144 over 8 GPUs), 20x20, 4 snakes, vision_range 5
-  cfg5  8 192 envs/GPU (65 536 over 8 GPUs), 40x40, 8 snakes, vision_range 5, frame_stack 4
+index, so ranks hold disjoint contiguous shards of one batch (no collective on
+the step path; the only collectives are the timing barrier and max-reduce).
+The metric's batch is fixed ("whole-node, 65536 envs ... 1->8 GPU"), so cfg3
+scales STRONG by default: 65 536 envs in all, 65 536 / N per GPU (8 192 at 8
+GPUs). --scaling weak keeps the per-GPU batch instead (65 536 per GPU).
+--config picks BASELINE.json's other configs (their presets are the per-GPU
+share of the 8-GPU configuration, weak scaling by default):
+  cfg2    4 096 envs/GPU, 20x20, 4 snakes, full-map observation
+  cfg3    65 536 envs in all (default), 20x20, 4 snakes, vision_range 5
+  cfg3s8  8 192 envs/GPU: cfg3's per-GPU shard at 8 GPUs, on one GPU
+  cfg4    32 768 envs/GPU (262 144 over 8 GPUs), 20x20, 4 snakes, vision_range 5
+  cfg5    8 192 envs/GPU (65 536 over 8 GPUs), 40x40, 8 snakes, vision_range 5, frame_stack 4
 
 A step = one SnakeVecEnv.step() over the GPU's whole batch. The timed region is
 exactly K steps between barrier + synchronize on both sides; value = all envs of
@@ -114,9 +125,45 @@ def spawn_bytes(S):
 PRESETS = {   # BASELINE.json configs (per GPU)
     'cfg2': dict(envs_per_gpu=4096, height=20, width=20, num_snakes=4, vision_range=0, frame_stack=1),
     'cfg3': dict(envs_per_gpu=65536, height=20, width=20, num_snakes=4, vision_range=5, frame_stack=1),
+    'cfg3s8': dict(envs_per_gpu=8192, height=20, width=20, num_snakes=4, vision_range=5, frame_stack=1),
     'cfg4': dict(envs_per_gpu=32768, height=20, width=20, num_snakes=4, vision_range=5, frame_stack=1),
     'cfg5': dict(envs_per_gpu=8192, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4),
 }
+# the whole-node batch of the configs whose batch is fixed (strong scaling by
+# default): BASELINE.json's metric, 65 536 envs over 1 -> 8 GPUs
+STRONG_TOTAL = {'cfg3': 65536}
+
+
+def batch_plan(config, scaling, world, envs_per_gpu, num_envs):
+    """(scaling, n_total) of a run: strong keeps the whole batch fixed (num_envs,
+    else the config's STRONG_TOTAL) and shards it over the ranks; weak runs
+    envs_per_gpu on every rank. Default: strong for the metric's config unless
+    the per-GPU batch was given, else weak."""
+    if scaling is None:
+        scaling = 'strong' if (num_envs is not None or (config in STRONG_TOTAL and envs_per_gpu is None)) else 'weak'
+    if scaling == 'strong':
+        n = num_envs if num_envs is not None else STRONG_TOTAL.get(config, PRESETS[config]['envs_per_gpu'])
+        if n < world:
+            raise SystemExit(f'--scaling strong: {n} envs cannot be sharded over {world} ranks')
+        return scaling, n
+    per = envs_per_gpu if envs_per_gpu is not None else PRESETS[config]['envs_per_gpu']
+    return scaling, per * world
+
+
+def launch_ranks(n, argv):
+    """--gpus N without a launcher: run this command line under
+    torch.distributed.run (N ranks on this node, rendezvous on 127.0.0.1) as a
+    child process and return its exit code. Called before torch touches the GPU;
+    the ranks inherit stdout, so rank 0's JSON line reaches the caller as is."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(n),
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    return subprocess.run(cmd, env=env).returncode
 
 
 def _cpu_worker(args):
@@ -162,7 +209,13 @@ def main():
     ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=200)
     ap.add_argument('--config', choices=sorted(PRESETS), default='cfg3')
-    ap.add_argument('--envs-per-gpu', type=int, default=None)
+    ap.add_argument('--envs-per-gpu', type=int, default=None,
+                    help='per-GPU batch (weak scaling; default: the preset\'s)')
+    ap.add_argument('--num-envs', type=int, default=None,
+                    help='whole-job batch, sharded over the ranks (strong scaling)')
+    ap.add_argument('--scaling', choices=('strong', 'weak'), default=None,
+                    help='strong: a fixed whole-job batch (default for cfg3, the metric\'s 65 536 envs); '
+                         'weak: a fixed per-GPU batch (default for the other presets)')
     ap.add_argument('--height', type=int, default=None)
     ap.add_argument('--width', type=int, default=None)
     ap.add_argument('--num-snakes', type=int, default=None)
@@ -191,11 +244,14 @@ def main():
                          '(0: none; default max(1, min(32, steps // 4)), so at least 4 launches are '
                          'averaged; a timed step costs ~1-2 us more: 0.1034 ms per step at stride 32 vs 0.1025 untimed, cfg3)')
     args = ap.parse_args()
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    scaling, n_total = batch_plan(args.config, args.scaling, world, args.envs_per_gpu, args.num_envs)
     for k, v in PRESETS[args.config].items():
         if getattr(args, k) is None:
             setattr(args, k, v)
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     env_kw = dict(height=args.height, width=args.width, snake_length=3,
                   vision_range=args.vision_range or None, frame_stack=args.frame_stack)
@@ -211,9 +267,6 @@ def main():
     import torch.distributed as dist
 
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit('--gpus N>1 needs one process per GPU: launch with torch.distributed.run')
     # under torch.distributed.run even one rank joins the process group, so the
     # RCCL barrier / device-side max-reduce of the N-GPU line runs on a 1-GPU box
     distributed = world > 1 or 'LOCAL_WORLD_SIZE' in os.environ
@@ -231,9 +284,8 @@ def main():
     from marlenv import SnakeVecEnv
     from marlenv import _native
 
-    per = args.envs_per_gpu
-    n_total = per * world
     lo, hi = shard_range(n_total, world, rank)
+    per = shard_range(n_total, world, 0)[1]   # (the largest shard: rank 0's)
     venv = SnakeVecEnv(hi - lo, num_snakes=S, device=device, seed=0, env_offset=lo,
                        spawn_background=args.spawn_background, spawn_ahead=args.spawn_ahead, **env_kw)
     venv.reset()
@@ -332,9 +384,12 @@ def main():
     value = n_total * args.steps / elapsed
     step_gbs = B * (hi - lo) / (elapsed / args.steps) / 1e9
     preset = PRESETS[args.config]
-    as_preset = all(getattr(args, k) == v for k, v in preset.items())
+    as_preset = all(getattr(args, k) == v for k, v in preset.items() if k != 'envs_per_gpu')
+    as_preset = as_preset and n_total == (STRONG_TOTAL.get(args.config, preset['envs_per_gpu']) if scaling == 'strong'
+                                          else preset['envs_per_gpu'] * world)
     name = args.config if as_preset else 'custom'
-    workload = (f'{name}: {per} envs/GPU x ({args.height}x{args.width}, {S} snakes, '
+    shard = f'{n_total} envs in all, {per} per GPU' if scaling == 'strong' else f'{per} envs/GPU'
+    workload = (f'{name}: {shard} x ({args.height}x{args.width}, {S} snakes, '
                 f'vision_range={args.vision_range or None}, frame_stack={args.frame_stack}), '
                 'random actions, all-done auto-reset in the step')
     line = {
@@ -346,7 +401,7 @@ def main():
         'warmup': args.warmup,
         'ms_per_step': round(elapsed / args.steps * 1e3, 4),
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': scaling,
         'vs_baseline': None,
         'dtype': 'u8',
         'data': 'synthetic (uniform random actions, seeded MT19937 envs)',
@@ -384,11 +439,11 @@ def main():
     if args.dump_dir:
         import numpy as np
         os.makedirs(args.dump_dir, exist_ok=True)
-        venv.sync()   # (after the last background spawn kernel, which writes env word 4)
+        venv.sync()   # (after the last background spawn kernel)
         keys, pos = venv.mt_state()
         np.savez(os.path.join(args.dump_dir, f'rank{rank}.npz'), lo=lo, hi=hi, world=world,
                  grids=venv.grids().cpu().numpy(), mt=keys.cpu().numpy(), mt_pos=pos.cpu().numpy(),
-                 env=venv.env_rec.view(hi - lo, 8).cpu().numpy(), obs=out[0].cpu().numpy(),
+                 env=venv.env_records().cpu().numpy(), obs=out[0].cpu().numpy(),
                  rew_sum=rsum.cpu().numpy())
     if rank == 0:
         print(json.dumps(line), flush=True)

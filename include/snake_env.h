@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 15
+#define SNAKE_ABI_VERSION 16
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -228,9 +228,20 @@ int snake_render_rgb(const snake_cfg *cfg, const snake_state *st, int64_t num_en
  * auto-resets run (kernel "resets": count only, every step); it waits for the
  * events. "resets_timed", "spawn_hits" and "spawn_jobs" count, while enabled,
  * the auto-resets, those that started from a ready spawn-ahead record and the
- * spawn-ahead attempts run. */
+ * spawn-ahead attempts run; "spawn_void", "reset_partial", "respawn_slow",
+ * "respawn_slow2", "gate_shut", "draw_wait" (resets that found a background job
+ * drawing their record and waited) and "draw_timeout" (... and gave up waiting,
+ * drawing from the env's own MT state) are further diagnostic counts. */
 int snake_timing_enable(int on);
 int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
+
+/* Testing aid (no reference counterpart), process-wide, read at each
+ * snake_step: "draw_wait_ticks" = how long (100 MHz ticks, default 200000 =
+ * 2 ms) an auto-reset waits for a background spawn-ahead job drawing its record
+ * before it voids the job and draws itself (0: never waits). Results are the
+ * same for any value. Returns SNAKE_E_ARG for an unknown name or a value out of
+ * range. */
+int snake_debug_set(const char *name, long long value);
 
 /* ---- Fused consumer: the reference's DQN forward on the observation batch
  * (train_dqn.py:104-151 DQN.forward / forward_features, train_ga.py:60-100),

@@ -1,19 +1,22 @@
 // snake_kernels.hip -- the batched multi-snake env step on CDNA4 (gfx950).
 //
-// One 64-lane wavefront (= one workgroup) per env instance or per reset worker.
-// snake_step = k_logic, then k_autoreset concurrently with k_encode:
-//   * k_logic: the env's current grid staged in LDS with 16-byte loads; the game
-//     rules (snake_env.py:301-374) lane-parallel, lane k = snake k: targets,
-//     collision groups (readlane broadcasts), the fruit-eater tail rule, rewards,
+// snake_step = k_logic, then one shared-phase launch (k_post / k_post_lean:
+// reset workers + encodes), with the spawn-ahead attempts in the step or in
+// k_spawn on the library's background streams (launch_step):
+//   * k_logic: 4, 8 or 16 lanes per env, the envs' current grids staged in LDS
+//     with 16-byte loads; the game rules (snake_env.py:301-374) lane-parallel,
+//     lane (env g, snake k): targets, collision groups (DPP moves inside the
+//     env's lane group), the fruit-eater tail rule, rewards,
 //     and a two-phase grid update (all tail clears, then all BODY/HEAD/TAIL
 //     writes) that reproduces the reference's snake-order update exactly
 //     ("two-phase update"); dead-body erase (prefix-scanned direction
 //     deque), fruit respawn (lane-chunked empty-cell ranking + MT19937 rejection
 //     sampling resolved by ballots); envs whose dones are all True are queued;
-//   * k_encode: the NHWC one-hot observation from the grid ring, 16-byte stores;
-//   * k_autoreset / k_reset: in-register MT19937 twist, Fisher-Yates draws in
-//     ballot-refined rounds recording a link table, pointer-chase trace of
-//     arr[:S], paint, fruits, encode.
+//   * encodes: the NHWC one-hot observation from the grid ring as table lookups
+//     (encode_tbl_block), 16-byte non-temporal stores;
+//   * reset workers / k_reset: in-register MT19937 twist, Fisher-Yates draws in
+//     ballot-refined rounds recording the draws, trace of arr[:S], paint,
+//     fruits, encode.
 // Compiled with -ffp-contract=off: rewards/statistics are float64 in the
 // reference's order of operations (snake_env.py:365-369, :385-389).
 #include <hip/hip_runtime.h>
@@ -63,6 +66,7 @@ __device__ unsigned long long g_resp_slow[kDiagSlots * kDiagSpread];    // k_log
 __device__ unsigned long long g_resp_slow2[kDiagSlots * kDiagSpread];   // ... (room, too few accepts among the prefetched raws)
 __device__ unsigned long long g_gate_shut[kDiagSlots * kDiagSpread];    // k_logic waves that found the background queue set busy
 __device__ unsigned long long g_draw_wait[kDiagSlots * kDiagSpread];    // resets that waited for a background job (DRAWING)
+__device__ unsigned long long g_draw_timeout[kDiagSlots * kDiagSpread]; // ... and gave up waiting (drew from the env's own state)
 #define DIAG_ADD(arr) atomicAdd(&(arr)[(blockIdx.x % kDiagSlots) * kDiagSpread], 1ull)
 
 #ifdef SNAKE_STAMPS
@@ -712,155 +716,6 @@ __device__ void perm_trace(int S, const NP *link, const lu16 *jsmall, int (&q)[M
     for (int k = 0; k < MS; k++) q[k] = bcast(x, k);
 }
 
-#ifdef SNAKE_DRAWBENCH
-// ------------------------------------------------ cooperative permutation draws
-// permutation(n)'s draws (the records of mt_perm_draws) on the kCoopW waves of
-// one workgroup: a round covers one aligned group of four key registers (256
-// raw words), wave w judging register 4g + w, instead of one wave's register
-// pair. The accept set is found by mt_perm_draws' bound refinement (accept iff
-// (w & mask) <= i - A_p, A_p = the accepts before word p), the prefix of the
-// counts of the waves before a wave exchanged through LDS once per refinement
-// pass: every wave writes its count, its open-word flag and the lane of the
-// bracket cut if its words hold it, one workgroup barrier, every wave reads all
-// four (two passes settle most rounds). Every wave holds the whole tempered key
-// (the twist runs on every wave: it is the same instructions, no latency lost)
-// and the round state i / mask / stream position, which all waves update the
-// same way from the exchanged counts. The waves of the workgroup must all call
-// it with the same MT state; they return with the same MT state and the
-// records written (the caller's barrier publishes them).
-// MEASURED SLOWER, kept for the diagnostic build only (scripts/attemptbench.py,
-// profiles/r05_attemptbench.json): identical records and poses, but a lone
-// attempt's draws take 2.1-2.5x the one-wave cycles (20x20, u16 record: 125 K
-// vs 42 K; 40x40: 356 K vs 144 K) -- a workgroup barrier and an LDS round trip
-// per refinement pass cost more than a whole one-wave round of ballots; with
-// k_post_lean's resets as four-wave groups (a reset without a record drawing
-// on all four) cfg5 went 0.1025 -> 0.1173 ms (profiles/r05_ab_coop_resets.jsonl).
-constexpr int kCoopW = 4;
-
-struct CoopXch {
-    uint4 *xb;   // LDS: [2][kCoopW] (ping-pong: a wave can be one exchange ahead)
-    int par;
-};
-
-// this wave's (cnt, und, cut) out, every wave's back (uniform values)
-__device__ __forceinline__ void coop_exch(CoopXch &x, int W, int cnt, int und, int cut, int (&ca)[kCoopW],
-                                          int (&ua)[kCoopW], int (&cuts)[kCoopW])
-{
-    uint4 *b = x.xb + x.par * kCoopW;
-    x.par ^= 1;
-    if ((threadIdx.x & (kWave - 1)) == 0) b[W] = make_uint4((uint32_t)cnt, (uint32_t)und, (uint32_t)cut, 0u);
-    // (LDS only: a workgroup fence would also drain the link-table atomics)
-    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#pragma unroll
-    for (int u = 0; u < kCoopW; u++) {
-        const uint4 v = b[u];
-        ca[u] = __builtin_amdgcn_readfirstlane((int)v.x);
-        ua[u] = __builtin_amdgcn_readfirstlane((int)v.y);
-        cuts[u] = __builtin_amdgcn_readfirstlane((int)v.z);
-    }
-}
-
-template <typename NP>
-__device__ void mt_perm_draws_coop(WaveMT &m, int n, int S, NP *link, int link_n, lu16 *jsmall, uint4 *xbuf,
-                                   int W, int lane)
-{
-    int i = n - 1;
-    if (i < 1) return;
-    uint32_t mask = gen_mask((uint32_t)i);
-    int lo = (int)(mask >> 1) + 1;
-    constexpr int kBig = 0x3fffffff;
-    CoopXch x{xbuf, 0};
-    NP *dummy = link + link_n + lane;
-    uint32_t my[3];   // this wave's register of each four-register group, tempered
-    auto select_key = [&]() {
-#pragma unroll
-        for (int g = 0; g < 3; g++) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int w = 0; w < kCoopW; w++)
-                if (4 * g + w < 10) v |= temper(m.w[4 * g + w]) & (0u - (uint32_t)(W == w));
-            my[g] = v;
-        }
-    };
-    select_key();
-    int ca[kCoopW], ua[kCoopW], cuts[kCoopW];
-    for (int guard = 0; i >= 1 && guard < (1 << 20); guard++) {
-        if (m.pos >= kMtN) {
-            mt_twist(m, lane);
-            select_key();
-        }
-#pragma unroll
-        for (int g = 0; g < 3; g++) {
-            // a round normally consumes the rest of the group; a bracket cut
-            // inside it repeats the group from the word after the cut
-            while (i >= 1 && m.pos < kMtN && (m.pos >> 8) == g) {
-                const int off = m.pos - 256 * g;                   // first unread word of the group
-                const int p = 64 * W + lane - off;                 // this word's offset in the round
-                const bool valid = p >= 0 && 256 * g + 64 * W + lane < kMtN;
-                const int v = valid ? (int)(my[g] & mask) : kBig;
-                // pass 0: the possible set; then alternate sure / possible sets
-                // from the other's prefix until they agree
-                unsigned long long c = __ballot(v <= i), a = 0ull;
-                const int k = i - lo + 1;                          // accepts left in this bracket
-                int cnt = __popcll(c);
-                coop_exch(x, W, cnt, 0, -1, ca, ua, cuts);
-                int bprev = 0;
-#pragma unroll
-                for (int u = 0; u < kCoopW; u++) bprev += (u < W) ? ca[u] : 0;
-                bool settled = false;
-                int b = 0;
-                for (int pass = 1; pass < 512 && !settled; pass++) {
-                    // the set from the previous pass gives this lane's prefix bound
-                    const unsigned long long prev = (pass & 1) ? c : a;
-                    b = mbcnt64(prev, bprev);
-                    const unsigned long long nw = __ballot(v + b <= i);
-                    if (pass & 1) a = nw; else c = nw;
-                    const int und = (a ^ c) != 0ull;
-                    cnt = __popcll(nw);
-                    // when this pass settles the round, nw == prev and bprev is
-                    // exact: the lane of the k-th accept of the round, if here
-                    int cut = -1;
-                    if (k - 1 - bprev >= 0 && k - 1 - bprev < cnt) {
-                        const unsigned long long hit = __ballot(inv_ballot(nw) && b == k - 1);
-                        cut = hit ? __ffsll((long long)hit) - 1 : -1;
-                    }
-                    coop_exch(x, W, cnt, und, cut, ca, ua, cuts);
-                    settled = (ua[0] | ua[1] | ua[2] | ua[3]) == 0;
-                    bprev = 0;
-#pragma unroll
-                    for (int u = 0; u < kCoopW; u++) bprev += (u < W) ? ca[u] : 0;
-                }
-                // a == c; b = the accepts before each word (bprev unchanged by the last pass)
-                int A = ca[0] + ca[1] + ca[2] + ca[3];
-                int wcut = kCoopW, lcut = 0;
-                const int end = min(256 * (g + 1), kMtN) - 256 * g;   // words of the group
-                int newoff = end;
-                if (A >= k) {   // the round ends right after the accept that leaves the bracket
-#pragma unroll
-                    for (int u = kCoopW - 1; u >= 0; u--)
-                        if (cuts[u] >= 0) { wcut = u; lcut = cuts[u]; }
-                    newoff = 64 * wcut + lcut + 1;
-                    A = k;
-                    if (W > wcut) a = 0ull;
-                    else if (W == wcut) a &= (2ull << lcut) - 1ull;
-                }
-                const int ii = i - b;
-                if constexpr (std::is_same<NP, lu16>::value) {
-                    *(inv_ballot(a) ? link + ii : dummy) = (uint16_t)v;
-                } else {
-                    if (inv_ballot(a)) perm_record(ii, v, S, link, jsmall);
-                }
-                m.pos = 256 * g + newoff;
-                i -= A;
-                mask = i > 0 ? (0xffffffffu >> __builtin_clz((uint32_t)i)) : 0u;
-                lo = (int)(mask >> 1) + 1;
-                if (newoff >= end) m.pos = min(256 * (g + 1), kMtN);
-            }
-        }
-    }
-}
-
-#endif  // SNAKE_DRAWBENCH
 
 // ------------------------------------------------------------ fruit respawn
 // random_empty_coords + grid[xs, ys] = FRUIT (grid_util.py:126-133,
@@ -1267,12 +1122,16 @@ __device__ __forceinline__ int load_reset_mt(const KCfg &c, const snake_state &s
 // instead of voiding it and drawing the same permutations again inline: the
 // job was queued at least a step earlier and is usually close to done, while an
 // inline 40x40 attempt took ~70-80 us of k_post_lean's span in a quarter of
-// cfg5's steps (round 5 kernel trace). The wait is bounded (kDrawWait ticks of
-// the 100 MHz clock, far beyond a job's ~100 us); after it the claim voids the
-// job as before and the reset draws from the env's own state -- right for a job
-// that started from a partial record too: the env's state is where that
-// record's failed permutations began, so the reset replays them.
-constexpr unsigned long long kDrawWait = 200000;   // 2 ms
+// cfg5's steps (round 5 kernel trace). The wait is bounded (KCfg.draw_wait ticks
+// of the 100 MHz clock, by default 2 ms, far beyond a job's ~100 us;
+// snake_debug_set("draw_wait_ticks") changes it, e.g. 0 for the test of the
+// fallback); after it the claim voids the job as before and the reset draws from
+// the env's own state -- right for a job that started from a partial record too:
+// the env's state is where that record's failed permutations began, so the reset
+// replays them. The voided job may still be drawing; it writes only its own
+// queue set's record buffer, which nothing reads until a later job of that set
+// (same stream, after it) publishes there, and its final compare-and-swap fails
+// against the claim's generation.
 __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &st, int64_t e, WaveMT &mt,
                                               int lane, uint32_t &cellw)
 {
@@ -1280,10 +1139,12 @@ __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &
     if (lane == 0) {
         uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + e * kEnvRec + ENV_SPAWN);
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long wait = (unsigned)c.draw_wait;
         if (c.diag && (ld_sc1(wp) & 3u) == SPAWN_DRAWING) DIAG_ADD(g_draw_wait);
-        while ((ld_sc1(wp) & 3u) == SPAWN_DRAWING && __builtin_amdgcn_s_memrealtime() - t0 < kDrawWait)
+        while ((ld_sc1(wp) & 3u) == SPAWN_DRAWING && __builtin_amdgcn_s_memrealtime() - t0 < wait)
             __builtin_amdgcn_s_sleep(8);
         v = (int)atomicAdd(wp, kGenOne);
+        if (c.diag && (v & 3) == SPAWN_DRAWING) DIAG_ADD(g_draw_timeout);
     }
     int spw = __shfl(v, 0);
     if ((spw & 3) == SPAWN_DRAWING) spw &= ~3;   // (still drawing: from the env's own state, as for NONE)
@@ -2057,11 +1918,7 @@ __global__ void __launch_bounds__(64 * WPB) k_logic(const KArgs)
 }
 
 
-// ---------------------------------------------------- step: the observation
-// Two kernels that run concurrently after k_logic (launch_step forks them onto
-// two streams): k_autoreset's workers run the queued auto-resets (latency-bound,
-// many registers, link table in LDS), k_encode encodes every other env's stacked
-// frames (bandwidth-bound, few registers: full occupancy).
+// ------------------------------------------------------- spawn-ahead records
 // Spawn-ahead job of env e (include/snake_env.h snake_step): one permutation
 // attempt of its next reset, from its MT state or its partial record, into the
 // record. k_logic queues only envs with no ready record whose reset is not this
@@ -2195,11 +2052,10 @@ __device__ void spawn_after_reset(const KCfg &c, const snake_state &st, int e, W
 }
 
 // ---------------------------------------------------- step: the observation
-// Two kernels that run concurrently after k_logic (launch_step forks them onto
-// two streams): k_autoreset's workers run the queued auto-resets (latency-bound,
-// many registers, link table in LDS) and then the queued spawn-ahead jobs,
-// k_encode encodes every other env's stacked frames (bandwidth-bound, few
-// registers: full occupancy).
+// After k_logic, one launch (k_post / k_post_lean, launch_step): reset workers
+// (the queued auto-resets, latency-bound, many registers, draw record in LDS,
+// then the in-step spawn-ahead jobs) and the encodes of every other env's
+// stacked frames (bandwidth-bound).
 // The observation of env e's current frame stack (_get_obs, snake_env.py:461-472):
 // the grid ring and crop centres staged in LDS, then the (staged) encode.
 __device__ __forceinline__ void encode_env(const KCfg &c, const snake_state &st, const snake_out &o, int e,
@@ -2829,6 +2685,7 @@ struct TimingRec {
 };
 std::mutex g_tmu;
 bool g_timing = false;
+int g_draw_wait_ticks = 200000;   // KCfg.draw_wait (snake_debug_set "draw_wait_ticks")
 std::vector<TimingRec> g_pending;
 std::vector<hipEvent_t> g_pool;
 std::map<std::string, std::pair<double, int64_t>> g_done;
@@ -3105,6 +2962,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
 {
     KCfg k = k0;
     k.diag = g_timing ? 1 : 0;
+    k.draw_wait = g_draw_wait_ticks;
     const hipStream_t sm = (hipStream_t)stream;
     DeviceGuard dg(sm);
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
@@ -3153,6 +3011,9 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         int *qc = st.resetq + (int64_t)k.qpar * (kNumQ * kQShards * k.q_cap + kQCounters) +
                   kNumQ * kQShards * k.q_cap;
         if (!spawn_launched) {
+            // (ordered after the set's previous k_spawn, which may still use its
+            // spawn and claim counters on its background stream)
+            if (bgc && bgc->pending[k.qpar]) (void)hipStreamWaitEvent(sm, bgc->done[k.qpar], 0);
             (void)hipMemsetAsync(qc, 0, sizeof(int) * kQSpGen * kQSpread, sm);   // (not the finished count)
         } else {
             (void)hipMemsetAsync(qc, 0, sizeof(int) * kQShards * kQSpread, sm);
@@ -3203,6 +3064,10 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         bgc->launched[k.qpar]++;
         bgc->steps++;
         if (hipEventRecord(bgc->done[k.qpar], bx) != hipSuccess) {
+            // (pending / done[] would not cover this k_spawn, which writes
+            // records, env word 4 and the set's counters: wait for it here so
+            // that snake_sync and the next steps need not)
+            (void)hipStreamSynchronize(bx);
             set_error("background spawn event failed");
             return fail(SNAKE_E_LAUNCH);
         }
@@ -3280,6 +3145,17 @@ extern "C" int snake_timing_enable(int on)
     return SNAKE_OK;
 }
 
+extern "C" int snake_debug_set(const char *name, long long value)
+{
+    if (name && !strcmp(name, "draw_wait_ticks") && value >= 0 && value <= INT_MAX) {
+        std::lock_guard<std::mutex> g(snake::g_tmu);
+        snake::g_draw_wait_ticks = (int)value;
+        return SNAKE_OK;
+    }
+    snake::set_error("snake_debug_set: unknown knob or value out of range");
+    return SNAKE_E_ARG;
+}
+
 extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *count)
 {
     if (!kernel || !total_ms || !count) {
@@ -3296,7 +3172,8 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
                     : !strcmp(kernel, "respawn_slow") ? (const void *)snake::g_resp_slow
                     : !strcmp(kernel, "respawn_slow2") ? (const void *)snake::g_resp_slow2
                     : !strcmp(kernel, "gate_shut") ? (const void *)snake::g_gate_shut
-                    : !strcmp(kernel, "draw_wait") ? (const void *)snake::g_draw_wait : nullptr;
+                    : !strcmp(kernel, "draw_wait") ? (const void *)snake::g_draw_wait
+                    : !strcmp(kernel, "draw_timeout") ? (const void *)snake::g_draw_timeout : nullptr;
     if (sym) {
         const int n = one ? 1 : snake::kDiagSlots * snake::kDiagSpread;
         std::vector<unsigned long long> v(n, 0ull), z(n, 0ull);
@@ -3333,108 +3210,9 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
 }
 
 #ifdef SNAKE_DRAWBENCH
-// Isolated draw benchmark: one permutation's draws on one wave, outside the
-// reset kernel's register pressure (cycles, final MT position).
-__global__ void k_drawbench(const uint32_t *mt_src, int pos0, int n, int S, unsigned long long *out)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int lane = threadIdx.x;
-    snake::lu16 *jarr = (snake::lu16 *)lds;   // the LDS draw record of the reset path
-    snake::WaveMT mt;
-    snake::mt_load(mt, mt_src, pos0, lane);
-    snake::wave_sync();
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    snake::mt_perm_draws(mt, n, S, jarr, n, jarr, lane);
-    snake::wave_sync();
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    int q[4];
-    snake::perm_trace_j<4>(S, n, jarr, q, lane);
-    snake::wave_sync();
-    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
-    if (lane == 0) { out[0] = t1 - t0; out[1] = (unsigned long long)mt.pos; out[2] = t2 - t1; out[3] = (unsigned long long)q[0]; }
-}
-
-// out_dev: [draw cycles, final MT position, trace cycles, arr[0]]
-extern "C" int snake_debug_drawbench(const uint32_t *mt_dev, int pos0, int n, int S, unsigned long long *out_dev)
-{
-    slaunch(k_drawbench, dim3(1), dim3(64), 2 * n + 256, 0, mt_dev, pos0, n, S, out_dev);
-    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
-}
-
-// One lone permutation attempt's draws (record cleared first where it needs
-// it) and trace: one wave (mt_perm_draws) or kCoopW waves (mt_perm_draws_coop),
-// the record kind JL as in spawn_attempt (1 u16 record, 2 u32 link table in
-// LDS, 0 u32 link table in global memory `gl`).
-// out: [cycles to the end of the draws, trace cycles, final MT position, arr[0..S)]
-template <bool COOP, int JL>
-__global__ void k_attemptbench(const uint32_t *mt_src, int pos0, int n, int S, uint32_t *gl, unsigned long long *out)
-{
-    using namespace snake;
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int lane = threadIdx.x & (kWave - 1), W = (int)(threadIdx.x >> 6);
-    uint4 *xb = reinterpret_cast<uint4 *>(lds);          // exchange slots
-    lu16 *jsmall = (lu16 *)(lds + 128);                   // S entries
-    uint8_t *rec = lds + 256;
-    const int stride = (n + 3) / 4 * 4 + kWave;           // (KCfg.link_stride)
-    WaveMT mt;
-    mt_load(mt, mt_src, pos0, lane);
-    __syncthreads();
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if constexpr (JL == 1) {
-        lu16 *jarr = (lu16 *)rec;
-        if (COOP) mt_perm_draws_coop(mt, n, S, jarr, n, jarr, xb, W, lane);
-        else mt_perm_draws(mt, n, S, jarr, n, jarr, lane);
-    } else if constexpr (JL == 2) {
-        lu32 *link = (lu32 *)rec;
-        for (int x = 4 * threadIdx.x; x < stride - kWave; x += 4 * blockDim.x) *(lu4 *)(link + x) = (v4u32)kNoLink;
-        __syncthreads();
-        if (COOP) mt_perm_draws_coop(mt, n, S, link, n, jsmall, xb, W, lane);
-        else mt_perm_draws(mt, n, S, link, n, jsmall, lane);
-    } else {
-        gu32 *link = (gu32 *)gl;
-        for (int x = 4 * threadIdx.x; x < stride - kWave; x += 4 * blockDim.x) *(gu4 *)(link + x) = (v4u32)kNoLink;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-        __syncthreads();
-        if (COOP) mt_perm_draws_coop(mt, n, S, link, n, jsmall, xb, W, lane);
-        else mt_perm_draws(mt, n, S, link, n, jsmall, lane);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    }
-    __syncthreads();
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    if (W != 0) return;
-    int q[4];
-    if constexpr (JL == 1) perm_trace_j<4>(S, n, (const lu16 *)rec, q, lane);
-    else if constexpr (JL == 2) perm_trace<4>(S, (const lu32 *)rec, jsmall, q, lane);
-    else perm_trace<4>(S, (const gu32 *)gl, jsmall, q, lane);
-    wave_sync();
-    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
-    if (lane == 0) {
-        out[0] = t1 - t0; out[1] = t2 - t1; out[2] = (unsigned long long)mt.pos;
-        for (int k = 0; k < 4; k++) out[3 + k] = (unsigned long long)q[k];
-    }
-}
-
-// coop: 0 one wave, 1 kCoopW waves; jl: 0/1/2; gl_dev: (n + 68) u32 for jl 0
-extern "C" int snake_debug_attemptbench(const uint32_t *mt_dev, int pos0, int n, int S, int coop, int jl,
-                                        uint32_t *gl_dev, unsigned long long *out_dev)
-{
-    using namespace snake;
-    if (S > 4) return -1;
-    const int stride = (n + 3) / 4 * 4 + kWave;
-    const int lds = 256 + (jl == 1 ? 2 * (n + kWave) : (jl == 2 ? 4 * stride : 0));
-    const dim3 g(1), b(coop ? kWave * kCoopW : kWave);
-    if (coop) {
-        if (jl == 1) slaunch((k_attemptbench<true, 1>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-        else if (jl == 2) slaunch((k_attemptbench<true, 2>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-        else slaunch((k_attemptbench<true, 0>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-    } else {
-        if (jl == 1) slaunch((k_attemptbench<false, 1>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-        else if (jl == 2) slaunch((k_attemptbench<false, 2>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-        else slaunch((k_attemptbench<false, 0>), g, b, lds, 0, mt_dev, pos0, n, S, gl_dev, out_dev);
-    }
-    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
-}
-
+// (diagnostic build only: the isolated draw / attempt benchmarks and the
+// cooperative four-wave draws they compare against, scripts/microbench/)
+#include "../../scripts/microbench/drawbench.inc"
 #endif
 
 #ifdef SNAKE_STAMPS

@@ -10,11 +10,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libsnake_amd.so')
 
-SNAKE_ABI_VERSION = 15
+SNAKE_ABI_VERSION = 16
 
 # Symbols include/snake_env.h declares (checked by tests/test_capi.py).
 EXPORTS = ('snake_plan', 'snake_build_candidates', 'snake_seed', 'snake_reset', 'snake_step',
-           'snake_sync', 'snake_release', 'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_last_error', 'snake_abi_version',
+           'snake_sync', 'snake_release', 'snake_render_rgb', 'snake_timing_enable', 'snake_timing_read', 'snake_debug_set', 'snake_last_error', 'snake_abi_version',
            'snake_dqn_plan', 'snake_dqn_rows', 'snake_dqn_forward', 'snake_dqn32_scratch', 'snake_dqn32_forward')
 
 
@@ -117,6 +117,7 @@ def lib(path=None):
     L.snake_dqn32_scratch.restype = I64
     L.snake_dqn32_forward.argtypes = [ctypes.POINTER(DqnCfg), ctypes.POINTER(Dqn32Net), P, I64, P, P, P, P]
     L.snake_timing_enable.argtypes = [ctypes.c_int]
+    L.snake_debug_set.argtypes = [ctypes.c_char_p, ctypes.c_longlong]
     L.snake_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_int64)]
     if L.snake_abi_version() != SNAKE_ABI_VERSION:
@@ -127,6 +128,11 @@ def lib(path=None):
 
 def timing_enable(on, L=None):
     check((L or lib()).snake_timing_enable(1 if on else 0), L)
+
+
+def debug_set(name, value, L=None):
+    """snake_debug_set (include/snake_env.h): a process-wide testing knob."""
+    check((L or lib()).snake_debug_set(name.encode(), int(value)), L)
 
 
 def timing_read(kernel, L=None):

@@ -373,23 +373,43 @@ class SnakeVecEnv:
         return self.env_rec.view(self.num_envs, 8)[:, 5]
 
     # ------------------------------------------------------- snapshot/restore
-    _STATE_BUFFERS = ('grid', 'snake', 'body', 'env_rec', 'ctr', 'stats', 'mt', 'spawn')
+    # The spawn-ahead records (snake_layout.spawn) and the status word that points
+    # at them (env word 4: status, record buffer, generation) are a cache of
+    # draws the next reset would make anyway (include/snake_env.h snake_step).
+    # With the background spawn kernel, which envs hold a record at a given
+    # moment depends on when each k_spawn ran, so snapshots hold the env state
+    # without the cache: word 4 in its canonical form 0 (no record; the next
+    # reset of the env draws from its MT19937 state, with identical results).
+    _STATE_BUFFERS = ('grid', 'snake', 'body', 'env_rec', 'ctr', 'stats', 'mt')
+
+    def env_records(self):
+        """(N, 8) int32 copy of the env records (alive_snakes, episode_length, ring
+        slot, MT position, spawn-ahead status, give-up flag, 0, 0) with word 4 in
+        its canonical form (0: no spawn-ahead record), ordered after the
+        background spawn kernel. Deterministic for any spawn-ahead mode, timing
+        and shard split."""
+        self.sync()
+        er = self.env_rec.view(self.num_envs, 8).clone()
+        er[:, 4] = 0
+        return er
 
     def state_dict(self, device=None):
-        """Snapshot of the whole batch: every persistent state buffer of
-        snake_layout (grid ring, snake records, body rings, env records, crop
-        centres, episode statistics, MT19937 keys, spawn-ahead records) copied
-        (to `device`, default: this env's device) plus the configuration it
-        belongs to. The step's queues and link tables are transient (empty
-        between steps) and not saved. load_state_dict() on this or a fresh
-        SnakeVecEnv of the same configuration continues bit-identically; the
-        tensors can be torch.save()d beside a learner checkpoint
-        (train_dqn.py:356-383)."""
+        """Snapshot of the whole batch: the persistent env state of snake_layout
+        (grid ring, snake records, body rings, env records, crop centres, episode
+        statistics, MT19937 keys) copied (to `device`, default: this env's device)
+        plus the configuration it belongs to. The spawn-ahead cache is not saved
+        (env word 4 canonical, env_records()), and the step's queues and link
+        tables are transient (empty between steps): two snapshots of the same env
+        state are equal whatever the spawn-ahead mode or timing. load_state_dict()
+        on this or a fresh SnakeVecEnv of the same configuration continues
+        bit-identically; the tensors can be torch.save()d beside a learner
+        checkpoint (train_dqn.py:356-383)."""
         torch = _torch()
         dev = torch.device(device) if device is not None else self.device
         self.sync()
+        sd = {k: getattr(self, k).detach().to(dev, copy=True) for k in self._STATE_BUFFERS if k != 'env_rec'}
+        sd['env_rec'] = self.env_records().view(-1).to(dev)
         torch.cuda.current_stream(self.device).synchronize()
-        sd = {k: getattr(self, k).detach().to(dev, copy=True) for k in self._STATE_BUFFERS}
         sd['meta'] = self._snapshot_meta()
         return sd
 
@@ -397,14 +417,14 @@ class SnakeVecEnv:
         lay = self.layout
         return dict(abi=int(self._L.snake_abi_version()), num_envs=self.num_envs,
                     cfg=[getattr(self.cfg, f) for f, _ in self.cfg._fields_
-                         if f != 'spawn_ahead'],
-                    sizes=[int(getattr(lay, k)) for k in ('grid', 'snake', 'body', 'env', 'ctr', 'stats',
-                                                          'mt', 'spawn')],
+                         if f not in ('spawn_ahead', 'spawn_background')],
+                    sizes=[int(getattr(lay, k)) for k in ('grid', 'snake', 'body', 'env', 'ctr', 'stats', 'mt')],
                     seed=self.seed_base, env_offset=self.env_offset, reset_done=self._reset_done)
 
     def load_state_dict(self, sd):
         """Restore a state_dict() snapshot (same configuration and num_envs,
-        checked); the next step continues exactly where the snapshot was taken."""
+        checked); the next step continues exactly where the snapshot was taken
+        (the spawn-ahead records are drawn afresh: env word 4 is 0)."""
         torch = _torch()
         mine, theirs = self._snapshot_meta(), sd['meta']
         for key in ('abi', 'num_envs', 'cfg', 'sizes'):
@@ -414,6 +434,7 @@ class SnakeVecEnv:
         with torch.cuda.device(self.device):
             for k in self._STATE_BUFFERS:
                 getattr(self, k).copy_(sd[k].to(self.device))
+            self.env_rec.view(self.num_envs, 8)[:, 4] = 0
         self.seed_base, self.env_offset = theirs['seed'], theirs['env_offset']
         self._reset_done = bool(theirs['reset_done'])
 

@@ -10,6 +10,7 @@ single-process one (digests all-gathered over gloo).
 import hashlib
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -88,3 +89,49 @@ def test_shard_range_tiles(n, world):
     assert rs[0][0] == 0 and rs[-1][1] == n
     assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
     assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
+
+
+def test_batch_plan_strong_and_weak():
+    """BASELINE.json's metric fixes the whole-node batch (65 536 envs over 1 -> 8
+    GPUs): cfg3 shards it (strong, 8 192 per GPU at 8 ranks) unless a per-GPU
+    batch is asked for; the other presets name a per-GPU share (weak)."""
+    for world in (1, 2, 4, 8):
+        sc, n = bench.batch_plan('cfg3', None, world, None, None)
+        assert (sc, n) == ('strong', 65536)
+        assert bench.shard_range(n, world, 0) == (0, 65536 // world)
+        assert bench.batch_plan('cfg3', 'weak', world, None, None) == ('weak', 65536 * world)
+        assert bench.batch_plan('cfg3', None, world, 1024, None) == ('weak', 1024 * world)
+        assert bench.batch_plan('cfg4', None, world, None, None) == ('weak', 32768 * world)
+        assert bench.batch_plan('cfg3s8', None, world, None, None) == ('weak', 8192 * world)
+        assert bench.batch_plan('cfg5', 'strong', world, None, None) == ('strong', 8192)
+        assert bench.batch_plan('cfg2', None, world, None, 1000) == ('strong', 1000)
+    assert bench.shard_range(65536, 8, 7) == (57344, 65536)
+    with pytest.raises(SystemExit):
+        bench.batch_plan('cfg3', 'strong', 8, None, 4)
+
+
+def test_bench_starts_its_ranks_without_a_launcher(monkeypatch):
+    """`bench.py --gpus N` with no WORLD_SIZE runs the same command line under
+    torch.distributed.run as a child (no exec, nothing touches the GPU first)
+    and exits with its return code."""
+    import subprocess
+    seen = {}
+
+    class Done:
+        returncode = 7
+
+    def fake_run(cmd, env=None, **kw):
+        seen['cmd'], seen['env'] = cmd, env
+        return Done()
+    monkeypatch.setattr(subprocess, 'run', fake_run)
+    monkeypatch.delenv('WORLD_SIZE', raising=False)
+    monkeypatch.setattr(sys, 'argv', ['bench.py', '--gpus', '2', '--dist-backend', 'gloo', '--steps', '3'])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 7
+    cmd = seen['cmd']
+    assert cmd[:3] == [sys.executable, '-m', 'torch.distributed.run']
+    assert cmd[cmd.index('--nproc-per-node') + 1] == '2' and cmd[cmd.index('--master-addr') + 1] == '127.0.0.1'
+    assert cmd[-6:] == ['--gpus', '2', '--dist-backend', 'gloo', '--steps', '3']
+    assert os.path.basename(cmd[-7]) == 'bench.py'
+    assert seen['env']['MASTER_ADDR'] == '127.0.0.1'

@@ -218,6 +218,11 @@ FULL_SIZE_CASES = {
     # 50x50 (26 000+ spawn poses): global link tables, in-step spawn-ahead, and
     # k_logic with one wave per workgroup (four would need 162 KB of LDS)
     'big50_16384': (16384, 4, 200, dict(height=50, width=50, snake_length=3, vision_range=4)),
+    # config 3's per-GPU shard under strong scaling at 8 GPUs (65 536 / 8): the
+    # last rank's envs (offset 57 344); batches of up to 8 192 envs default to
+    # the background spawn kernel (two library streams, 512 reset / spawn
+    # workers, threshold 4): this is that default at its boundary
+    'cfg3s8_8192': (8192, 4, 400, dict(height=20, width=20, snake_length=3, vision_range=5), 57344),
 }
 
 
@@ -228,13 +233,14 @@ def test_full_size_sampled_parity(oracle, case):
     the bench times (past 200 steps almost every reset starts from a spawn-ahead
     record)."""
     from marlenv import SnakeVecEnv
-    N, S, T, kw = FULL_SIZE_CASES[case]
+    N, S, T, kw = FULL_SIZE_CASES[case][:4]
+    off = FULL_SIZE_CASES[case][4] if len(FULL_SIZE_CASES[case]) > 4 else 0
     vr = kw['vision_range']
-    v = SnakeVecEnv(N, num_snakes=S, seed=0, **kw)
+    v = SnakeVecEnv(N, num_snakes=S, seed=0, env_offset=off, **kw)
     obs = v.reset()
     idx = np.unique(np.concatenate([np.arange(8), np.linspace(0, N - 1, 40).astype(int),
                                     np.random.RandomState(0).randint(0, N, 16)]))
-    refs = {int(i): oracle.OracleEnv(seed=int(i), num_snakes=S, **kw) for i in idx}
+    refs = {int(i): oracle.OracleEnv(seed=off + int(i), num_snakes=S, **kw) for i in idx}
     o0 = obs[torch.from_numpy(idx).cuda()].cpu().numpy()
     for row, i in enumerate(idx):
         assert (refs[int(i)].reset() == o0[row]).all()
@@ -262,6 +268,9 @@ def test_full_size_sampled_parity(oracle, case):
         assert int(heads[~alive].sum()) == 0
         assert not bool(info['error'].any())
     assert n_ep > 0.005 * N * T / 60
+    if case == 'cfg3s8_8192':   # (two spawn record buffers per env: the background kernel's default here)
+        assert v.layout.spawn == 2 * N * 672 * 4
+    v.close()
 
 
 @pytest.mark.parametrize('S,kw,spawn', [
@@ -510,6 +519,39 @@ def test_snapshot_restore_roundtrip(kw, S):
     bad = SnakeVecEnv(N // 2, num_snakes=S, seed=31, **kw)
     with pytest.raises(ValueError):
         bad.load_state_dict(snap)
+
+
+def test_snapshot_is_canonical():
+    """Snapshots hold the env state, not the spawn-ahead cache: twins stepped
+    with the background spawn kernel, the in-step spawn-ahead and none at all
+    give equal state_dicts (the background one's records depend on when each
+    k_spawn ran), and a snapshot loads into an env of another spawn-ahead mode
+    and continues bit-identically."""
+    from marlenv import SnakeVecEnv
+    N, S = 512, 4
+    kw = dict(height=20, width=20, vision_range=5)
+    modes = [dict(spawn_background=1), dict(spawn_background=-1), dict(spawn_ahead=-1, spawn_background=-1)]
+    envs = [SnakeVecEnv(N, num_snakes=S, seed=3, **m, **kw) for m in modes]
+    for v in envs:
+        v.reset()
+    g = torch.Generator(device='cuda').manual_seed(6)
+    acts = torch.randint(0, 3, (90, N, S), generator=g, device='cuda', dtype=torch.int8)
+    for t in range(50):
+        for v in envs:
+            v.step(acts[t])
+    sds = [v.state_dict(device='cpu') for v in envs]
+    for sd in sds[1:]:
+        for k in SnakeVecEnv._STATE_BUFFERS:
+            assert torch.equal(sds[0][k], sd[k]), k
+    assert int(sds[0]['env_rec'].view(N, 8)[:, 4].abs().sum()) == 0
+    other = SnakeVecEnv(N, num_snakes=S, seed=0, **modes[1], **kw)
+    other.load_state_dict(sds[0])
+    for t in range(50, 90):
+        a, b = envs[0].step(acts[t]), other.step(acts[t])
+        for x, y in zip(a[:3], b[:3]):
+            assert torch.equal(x, y), t
+    for v in envs + [other]:
+        v.close()
 
 
 def test_vec_env_on_non_current_device():
@@ -769,9 +811,46 @@ def test_background_overlap_stress(kw):
     hits, voids = _native.timing_read('spawn_hits')[1], _native.timing_read('spawn_void')[1]
     bg.sync()
     assert torch.equal(bg.grids(), ref.grids()) and torch.equal(bg.mt, ref.mt)
-    er_b, er_r = bg.env_rec.view(N, 8), ref.env_rec.view(N, 8)
-    assert torch.equal(er_b[:, :4], er_r[:, :4])   # (word 4, the spawn-ahead status, is mode bookkeeping)
+    assert torch.equal(bg.env_records(), ref.env_records())   # (all eight words, word 4 canonical)
     assert hits > 0 and voids > 0, (hits, voids)
+    bg.close()
+    ref.close()
+
+
+def test_draw_wait_fallback():
+    """The bounded DRAWING wait's fallback (claim_reset_mt): with the wait at 0
+    ticks (snake_debug_set "draw_wait_ticks") every auto-reset that finds a
+    background job drawing its record voids the job at once and draws from the
+    env's own MT state while the job is still running. The rollout must still
+    equal the in-step spawn-ahead run bit for bit, and the fallback must have
+    been taken (the "draw_timeout" count)."""
+    from marlenv import SnakeVecEnv, _native
+    N, S = 384, 8
+    kw = dict(height=40, width=40, vision_range=5, num_fruits=24)
+    bg = SnakeVecEnv(N, num_snakes=S, seed=23, spawn_ahead=8, spawn_background=1, **kw)
+    ref = SnakeVecEnv(N, num_snakes=S, seed=23, spawn_ahead=-1, spawn_background=-1, **kw)
+    assert torch.equal(bg.reset(), ref.reset())
+    g = torch.Generator(device='cuda').manual_seed(9)
+    for k in ('draw_wait', 'draw_timeout'):
+        _native.timing_read(k)
+    _native.debug_set('draw_wait_ticks', 0)
+    try:
+        _native.timing_enable(True)
+        for t in range(160):
+            a = torch.randint(0, 3, (N, S), generator=g, device='cuda', dtype=torch.int8)
+            ob, rb, db, ib = bg.step(a)
+            orf, rr, dr, ir = ref.step(a)
+            assert torch.equal(ob, orf) and torch.equal(rb, rr) and torch.equal(db, dr), f'step {t}'
+        _native.timing_enable(False)
+    finally:
+        _native.timing_enable(False)
+        _native.debug_set('draw_wait_ticks', 200000)
+    waits, timeouts = _native.timing_read('draw_wait')[1], _native.timing_read('draw_timeout')[1]
+    assert torch.equal(bg.grids(), ref.grids()) and torch.equal(bg.mt, ref.mt)
+    assert torch.equal(bg.env_records(), ref.env_records())
+    assert timeouts > 0 and timeouts == waits, (waits, timeouts)
+    with pytest.raises(Exception):
+        _native.debug_set('no_such_knob', 1)
     bg.close()
     ref.close()
 

@@ -63,12 +63,9 @@ def test_two_ranks_equal_one_process(tmp_path, config, per, bg):
     parts = [np.load(two / f'rank{r}.npz') for r in range(2)]
     assert [(int(p['lo']), int(p['hi'])) for p in parts] == [(0, per), (per, 2 * per)]
     for key in ('grids', 'mt', 'mt_pos', 'env', 'obs', 'rew_sum'):
+        # (all eight env record words: bench.py dumps SnakeVecEnv.env_records(),
+        # the spawn-ahead status word in its canonical form)
         cat, ref = np.concatenate([p[key] for p in parts]), full[key]
-        if key == 'env' and bg >= 0:
-            # background spawn-ahead: the status word (ENV_SPAWN, word 4: record
-            # status + generation) depends on when each k_spawn finished relative
-            # to the steps -- bookkeeping, not env state
-            cat, ref = np.delete(cat, 4, axis=1), np.delete(ref, 4, axis=1)
         assert cat.tobytes() == ref.tobytes(), key
     if config == 'cfg3':   # the rollout went through episode ends (auto-resets on both ranks)
         assert all(int(p['env'][:, 1].min()) < 50 for p in parts)
@@ -93,3 +90,32 @@ def test_rccl_rank_equals_plain_process(tmp_path):
     a, b = np.load(r / 'rank0.npz'), np.load(one / 'rank0.npz')
     for key in ('grids', 'mt', 'mt_pos', 'env', 'obs', 'rew_sum'):
         assert a[key].tobytes() == b[key].tobytes(), key
+
+
+@pytest.mark.timeout(600)
+def test_strong_scaling_self_launched(tmp_path):
+    """`bench.py --gpus 2` with no launcher in front (no WORLD_SIZE): bench.py
+    starts its two ranks itself under torch.distributed.run and relays rank 0's
+    line. Strong scaling: the fixed whole-job batch (--num-envs) is split into
+    two shards, and their concatenated results equal one process stepping the
+    whole batch -- every env record word included (the spawn-ahead status word
+    is dumped in its canonical form, SnakeVecEnv.env_records)."""
+    n = 1536
+    common = ['--steps', '40', '--warmup', '10', '--no-cpu-baseline', '--timing-stride', '4',
+              '--global-actions', '--config', 'cfg3', '--num-envs', str(n)]
+    two = tmp_path / 'two'
+    lines = _run([sys.executable, 'bench.py', '--gpus', '2', '--dist-backend', 'gloo', '--dump-dir', str(two)] + common,
+                 tmp_path, 'two')
+    assert len(lines) == 1, 'rank 0 prints exactly one JSON line'
+    line = lines[0]
+    assert line['n_gpus'] == 2 and line['scaling'] == 'strong' and line['process_group'] == 'gloo'
+    assert line['config']['num_envs'] == n and line['config']['envs_per_gpu'] == n // 2
+    one = tmp_path / 'one'
+    lines1 = _run([sys.executable, 'bench.py', '--dump-dir', str(one)] + common, tmp_path, 'one')
+    assert len(lines1) == 1 and lines1[0]['n_gpus'] == 1 and lines1[0]['scaling'] == 'strong'
+    full = np.load(one / 'rank0.npz')
+    parts = [np.load(two / f'rank{r}.npz') for r in range(2)]
+    assert [(int(p['lo']), int(p['hi'])) for p in parts] == [(0, n // 2), (n // 2, n)]
+    for key in ('grids', 'mt', 'mt_pos', 'env', 'obs', 'rew_sum'):
+        cat = np.concatenate([p[key] for p in parts])
+        assert cat.tobytes() == full[key].tobytes(), key
