@@ -238,8 +238,10 @@ int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
 /* Testing aid (no reference counterpart), process-wide, read at each
  * snake_step: "draw_wait_ticks" = how long (100 MHz ticks, default 200000 =
  * 2 ms) an auto-reset waits for a background spawn-ahead job drawing its record
- * before it voids the job and draws itself (0: never waits). Results are the
- * same for any value. Returns SNAKE_E_ARG for an unknown name or a value out of
+ * before it voids the job and draws itself (0: never waits); "spawn_delay_ticks"
+ * = fault injection: each background job sleeps that long (default 0) once it
+ * has marked a record DRAWING, so resets meet jobs in flight. Results are the
+ * same for any values. Returns SNAKE_E_ARG for an unknown name or a value out of
  * range. */
 int snake_debug_set(const char *name, long long value);
 

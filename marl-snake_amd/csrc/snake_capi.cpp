@@ -533,7 +533,11 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // cfg2: 0.0397 -> 0.0391 ms, same box; 256: 0.0392), 2 048 on 40x40 (cfg5:
     // 512 0.0827-0.0832, 1 024 0.0822, 2 048 0.0823)
     k->spawn_slots = (int)std::min<int64_t>(N, bg_small ? 512 : kResetSlots);
-    k->bg_tries = 1;   // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
+#ifndef SNAKE_BG_TRIES_SMALL
+#define SNAKE_BG_TRIES_SMALL 1
+#endif
+    // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
+    k->bg_tries = bg_small ? SNAKE_BG_TRIES_SMALL : 1;
     k->spawn_tries = 1;   // attempts per in-step spawn-ahead job (2 measured cfg3 0.0875 -> 0.103 ms: a retry doubles the chain)
     k->lds_obs_bytes = off;
     {

@@ -99,6 +99,7 @@ struct KCfg {
     int spawn_tries;            // in-step spawn-ahead jobs: permutation attempts per job (until disjoint)
     uint32_t spawn_gate;        // bg: k_spawn launches on this step's queue set so far (kQSpGen)
     int draw_wait;              // bg: 100 MHz ticks a reset waits for a record being drawn (claim_reset_mt)
+    int spawn_delay;            // bg: 100 MHz ticks a k_spawn job sleeps once it marks a record DRAWING (tests)
     // lean encode (encode_lean): the frames copied into a zero-bordered LDS image
     // (lp columns / vr rows of padding, pw bytes per row, pframe bytes per frame)
     // so the crop needs no bounds test; unit -> (snake, row, col, frame) by

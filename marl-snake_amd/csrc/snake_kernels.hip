@@ -2015,6 +2015,12 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
         if (!__shfl(won, 0)) return;
         spw = (spw & ~3u) | SPAWN_DRAWING;
     }
+    // (fault injection for the tests, snake_debug_set "spawn_delay_ticks": the
+    // job holds the record DRAWING that much longer, so resets meet it)
+    if (c.spawn_delay) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned)c.spawn_delay) __builtin_amdgcn_s_sleep(32);
+    }
     const int buf = (spw >> 2) & 1;
     WaveMT mt;
     if (st0 != SPAWN_NONE) {
@@ -2686,6 +2692,7 @@ struct TimingRec {
 std::mutex g_tmu;
 bool g_timing = false;
 int g_draw_wait_ticks = 200000;   // KCfg.draw_wait (snake_debug_set "draw_wait_ticks")
+int g_spawn_delay_ticks = 0;      // KCfg.spawn_delay (snake_debug_set "spawn_delay_ticks")
 std::vector<TimingRec> g_pending;
 std::vector<hipEvent_t> g_pool;
 std::map<std::string, std::pair<double, int64_t>> g_done;
@@ -2822,7 +2829,9 @@ static BgCtx *bg_ctx(const snake_state &st, bool create)
     BgCtx c;
     if (hipStreamCreateWithFlags(&c.x[0], hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c.x[1], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c.fork, kJoinFlags) != hipSuccess ||
+        // (the fork event rides on k_logic's dispatch as its stop event, like
+        // the timing events: a timing-capable event without the system fence)
+        hipEventCreateWithFlags(&c.fork, hipEventDisableSystemFence) != hipSuccess ||
         hipEventCreateWithFlags(&c.done[0], kJoinFlags) != hipSuccess ||
         hipEventCreateWithFlags(&c.done[1], kJoinFlags) != hipSuccess) {
         destroy_bg(c);
@@ -2963,6 +2972,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     KCfg k = k0;
     k.diag = g_timing ? 1 : 0;
     k.draw_wait = g_draw_wait_ticks;
+    k.spawn_delay = g_spawn_delay_ticks;
     const hipStream_t sm = (hipStream_t)stream;
     DeviceGuard dg(sm);
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
@@ -2980,6 +2990,16 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         k.spawn_gate = bgc->launched[k.qpar];
     }
     TimedLaunch t1("k_logic", sm);
+    // Background spawn-ahead: the fork onto the background stream is k_logic's
+    // own dispatch -- its stop event (the timing event when the launch is timed)
+    // -- not an event record of its own on the caller's stream: that marker
+    // packet stood between k_logic and k_post, 5.3 us of idle GPU per step at
+    // 8 192 envs (round 6 kernel trace).
+    hipEvent_t fork_ev = nullptr;
+    if (bgc) {
+        if (!t_ev1) t_ev1 = bgc->fork;
+        fork_ev = t_ev1;
+    }
     const KArgs la{k, st, o, actions};
     // four waves (groups) per workgroup where their LDS fits (KCfg.logic_wpb):
     // k_logic cfg4 20.4 -> 19.4 us, cfg5 21.9 -> 21.1 against one (round 4)
@@ -2998,6 +3018,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     };
     if (k.logic_wpb == 4) launch_logic(std::integral_constant<int, 4>{});
     else launch_logic(std::integral_constant<int, 1>{});
+    if (bgc && fork_ev == bgc->fork) t_ev1 = nullptr;
     t1.close();
     int rc = check_launch("k_logic");
     if (rc) return rc;
@@ -3041,9 +3062,10 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     }
     if (bgc) {
         // this step's spawn kernel on the background stream once k_logic has
-        // passed; not joined (the k_logic two steps later waits for it)
+        // passed (its dispatch's stop event, above); not joined (k_logic two
+        // steps later only queues into the set once it has finished)
         hipStream_t bx = bgc->x[k.qpar];
-        if (hipEventRecord(bgc->fork, sm) != hipSuccess || hipStreamWaitEvent(bx, bgc->fork, 0) != hipSuccess) {
+        if (hipStreamWaitEvent(bx, fork_ev, 0) != hipSuccess) {
             set_error("fork to the background stream failed");
             return fail(SNAKE_E_LAUNCH);
         }
@@ -3147,10 +3169,10 @@ extern "C" int snake_timing_enable(int on)
 
 extern "C" int snake_debug_set(const char *name, long long value)
 {
-    if (name && !strcmp(name, "draw_wait_ticks") && value >= 0 && value <= INT_MAX) {
+    if (name && value >= 0 && value <= INT_MAX) {
         std::lock_guard<std::mutex> g(snake::g_tmu);
-        snake::g_draw_wait_ticks = (int)value;
-        return SNAKE_OK;
+        if (!strcmp(name, "draw_wait_ticks")) { snake::g_draw_wait_ticks = (int)value; return SNAKE_OK; }
+        if (!strcmp(name, "spawn_delay_ticks")) { snake::g_spawn_delay_ticks = (int)value; return SNAKE_OK; }
     }
     snake::set_error("snake_debug_set: unknown knob or value out of range");
     return SNAKE_E_ARG;

@@ -35,6 +35,7 @@ def main():
     from marlenv import SnakeVecEnv
     out = {}
     for name, N, kw in (('cfg2', 4096, dict(height=20, width=20)),
+                        ('cfg3s8', 8192, dict(height=20, width=20, vision_range=5)),
                         ('cfg3', 65536, dict(height=20, width=20, vision_range=5))):
         v = SnakeVecEnv(N, num_snakes=4, seed=0, **kw)
         v.reset()

@@ -19,6 +19,11 @@ FLAGS = ['-O3', '-std=c++17', '-ffp-contract=off', '--offload-arch=gfx950', '-ml
          '-amdgpu-atomic-optimizer-strategy=None', '--cuda-device-only']
 
 
+def demangle(name):
+    r = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-cxxfilt', name], capture_output=True, text=True)
+    return r.stdout.strip().replace('snake::', '') or name
+
+
 def main():
     with tempfile.TemporaryDirectory() as d:
         asm = os.path.join(d, 'k.s')
@@ -44,7 +49,7 @@ def main():
         if not u:
             continue
         print(json.dumps({
-            'kernel': re.sub(r'^_ZN5snake', '', name)[:48],
+            'kernel': demangle(name),
             'instructions': len(ins),
             'v_writelane': sum(i.startswith('v_writelane') for i in ins),
             'v_readlane': sum(i.startswith('v_readlane') for i in ins),

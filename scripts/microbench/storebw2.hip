@@ -1,0 +1,113 @@
+// Store-bandwidth ceiling for the observation write, by store width and cache
+// policy (round 6). Every wave writes SEG consecutive bytes (its "envs"), lane l
+// at seg + i * 64 * W + l * W, W = 4, 8 or 16 bytes per lane; policies: plain
+// (write-back), nt (non-temporal), sc0 sc1 (write-through, inline asm), with
+// 1, 2 or 4 waves per workgroup and an LDS pad that caps waves per CU. Also a
+// read-then-write pass (every wave first reads RB bytes of its own input, like
+// an encode's grid read, then writes). 254 MB per pass (cfg3's observations per
+// step), four buffers in turn.
+//   hipcc -O3 --offload-arch=gfx950 -o storebw2 storebw2.hip && ./storebw2
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+template <int W, int POL>
+__device__ __forceinline__ void st(uint8_t *p, uint32_t x)
+{
+    if constexpr (W == 16) {
+        const v4u v = (v4u){x, x + 1, x + 2, x + 3};
+        if constexpr (POL == 0) *reinterpret_cast<v4u *>(p) = v;
+        else if constexpr (POL == 1) __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
+        else __asm__ volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    } else if constexpr (W == 8) {
+        const v2u v = (v2u){x, x + 1};
+        if constexpr (POL == 0) *reinterpret_cast<v2u *>(p) = v;
+        else if constexpr (POL == 1) __builtin_nontemporal_store(v, reinterpret_cast<v2u *>(p));
+        else __asm__ volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    } else {
+        if constexpr (POL == 0) *reinterpret_cast<uint32_t *>(p) = x;
+        else if constexpr (POL == 1) __builtin_nontemporal_store(x, reinterpret_cast<uint32_t *>(p));
+        else __asm__ volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+    }
+}
+
+template <int W, int POL>
+__global__ void k_seg(uint8_t *out, const uint8_t *in, int64_t total, int seg, int rb)
+{
+    extern __shared__ uint8_t lds[];
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t base = wave * seg;
+    if (base >= total) return;
+    uint32_t acc = 0;
+    if (rb) {   // read this wave's input first (16 B per lane), as an encode reads its grids
+        const v4u *src = reinterpret_cast<const v4u *>(in + wave * rb);
+        for (int c = lane; c < rb / 16; c += 64) {
+            const v4u v = src[c];
+            acc += v.x ^ v.y ^ v.z ^ v.w;
+        }
+        if (acc == 0x12345678u) lds[0] = 1;   // (keeps the loads)
+    }
+    const int n = seg / W;
+    for (int c = lane; c < n; c += 64) st<W, POL>(out + base + (int64_t)c * W, (uint32_t)c + acc);
+}
+
+int main()
+{
+    const int64_t bytes = 65536LL * 3872;   // 253.8 MB
+    uint8_t *buf, *in;
+    (void)hipMalloc(&buf, 4 * bytes + 65536);
+    (void)hipMalloc(&in, 65536LL * 512 + 65536);
+    (void)hipMemset(in, 1, 65536LL * 512);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    int it = 0;
+    auto timeit = [&](const char *name, auto launch0) {
+        for (int i = 0; i < 3; i++) launch0(buf + (int64_t)(it++ & 3) * bytes);
+        hipDeviceSynchronize();
+        const int R = 20;
+        hipEventRecord(a);
+        for (int i = 0; i < R; i++) launch0(buf + (int64_t)(it++ & 3) * bytes);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        ms /= R;
+        printf("%-56s %8.2f us  %6.2f TB/s\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e12);
+        fflush(stdout);
+    };
+    auto run = [&](auto wc, auto pc) {
+        constexpr int W = decltype(wc)::value, POL = decltype(pc)::value;
+        const char *pn = POL == 0 ? "wb" : (POL == 1 ? "nt" : "sc01");
+        for (int seg : {3872 * 4, 4096, 65536})
+            for (int wpb : {1, 4})
+                for (int lds : {0, 16384})
+                    for (int rb : {0, 1600}) {
+                        if (seg % W || (rb && seg != 3872 * 4)) continue;
+                        const int64_t waves = (bytes + seg - 1) / seg;
+                        const int64_t blocks = (waves + wpb - 1) / wpb;
+                        char nm[160];
+                        snprintf(nm, sizeof nm, "W%2d %-4s seg %6d wpb %d lds %5d rb %4d", W, pn, seg, wpb, lds * wpb, rb);
+                        timeit(nm, [&](uint8_t *o) {
+                            hipLaunchKernelGGL((k_seg<W, POL>), dim3((unsigned)blocks), dim3(64 * wpb), lds * wpb, 0, o, in,
+                                               bytes, seg, rb);
+                        });
+                    }
+    };
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
+    using I16 = std::integral_constant<int, 16>;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    run(I16{}, P0{}); run(I16{}, P1{}); run(I16{}, P2{});
+    run(I8{}, P0{});  run(I8{}, P1{});
+    run(I4{}, P0{});  run(I4{}, P1{});
+    (void)hipFree(buf);
+    (void)hipFree(in);
+    return 0;
+}

@@ -20,8 +20,9 @@ from marlenv import SnakeVecEnv, _native  # noqa: E402
 CFGS = {'cfg3': (65536, 4, dict(height=20, width=20, vision_range=5)),
         'cfg4': (32768, 4, dict(height=20, width=20, vision_range=5)),
         'cfg2': (4096, 4, dict(height=20, width=20)),
+        'cfg3s8': (8192, 4, dict(height=20, width=20, vision_range=5)),
         'cfg5': (8192, 8, dict(height=40, width=40, vision_range=5, frame_stack=4))}
-KEYS = ('resets_timed', 'spawn_hits', 'reset_partial', 'spawn_jobs', 'spawn_void', 'respawn_slow', 'respawn_slow2', 'gate_shut', 'draw_wait')
+KEYS = ('resets_timed', 'spawn_hits', 'reset_partial', 'spawn_jobs', 'spawn_void', 'respawn_slow', 'respawn_slow2', 'gate_shut', 'draw_wait', 'draw_timeout')
 
 
 def main():

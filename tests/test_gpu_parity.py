@@ -817,13 +817,17 @@ def test_background_overlap_stress(kw):
     ref.close()
 
 
-def test_draw_wait_fallback():
-    """The bounded DRAWING wait's fallback (claim_reset_mt): with the wait at 0
-    ticks (snake_debug_set "draw_wait_ticks") every auto-reset that finds a
-    background job drawing its record voids the job at once and draws from the
-    env's own MT state while the job is still running. The rollout must still
-    equal the in-step spawn-ahead run bit for bit, and the fallback must have
-    been taken (the "draw_timeout" count)."""
+@pytest.mark.parametrize('wait', [0, 200000])
+def test_draw_wait_fallback(wait):
+    """The DRAWING wait of claim_reset_mt and its fallback, with background jobs
+    held DRAWING for 300 us each (snake_debug_set "spawn_delay_ticks", fault
+    injection) so that resets meet them: with the default wait (2 ms) such a
+    reset waits for the job's record; with the wait at 0 ticks it voids the job
+    at once and draws from the env's own MT state while the job is still running
+    (and later writes its queue set's record buffer). Either way the rollout
+    equals the in-step spawn-ahead run bit for bit, and the counters show the
+    path was taken ("draw_wait": resets that met a job drawing; "draw_timeout":
+    those that gave up waiting)."""
     from marlenv import SnakeVecEnv, _native
     N, S = 384, 8
     kw = dict(height=40, width=40, vision_range=5, num_fruits=24)
@@ -833,7 +837,8 @@ def test_draw_wait_fallback():
     g = torch.Generator(device='cuda').manual_seed(9)
     for k in ('draw_wait', 'draw_timeout'):
         _native.timing_read(k)
-    _native.debug_set('draw_wait_ticks', 0)
+    _native.debug_set('draw_wait_ticks', wait)
+    _native.debug_set('spawn_delay_ticks', 30000)
     try:
         _native.timing_enable(True)
         for t in range(160):
@@ -841,14 +846,17 @@ def test_draw_wait_fallback():
             ob, rb, db, ib = bg.step(a)
             orf, rr, dr, ir = ref.step(a)
             assert torch.equal(ob, orf) and torch.equal(rb, rr) and torch.equal(db, dr), f'step {t}'
-        _native.timing_enable(False)
+        bg.sync()
+        torch.cuda.synchronize()
     finally:
         _native.timing_enable(False)
         _native.debug_set('draw_wait_ticks', 200000)
+        _native.debug_set('spawn_delay_ticks', 0)
     waits, timeouts = _native.timing_read('draw_wait')[1], _native.timing_read('draw_timeout')[1]
     assert torch.equal(bg.grids(), ref.grids()) and torch.equal(bg.mt, ref.mt)
     assert torch.equal(bg.env_records(), ref.env_records())
-    assert timeouts > 0 and timeouts == waits, (waits, timeouts)
+    assert waits > 0, (waits, timeouts)
+    assert timeouts == (waits if wait == 0 else 0), (waits, timeouts)
     with pytest.raises(Exception):
         _native.debug_set('no_such_knob', 1)
     bg.close()
