@@ -240,8 +240,11 @@ int snake_timing_read(const char *kernel, double *total_ms, int64_t *count);
  * 2 ms) an auto-reset waits for a background spawn-ahead job drawing its record
  * before it voids the job and draws itself (0: never waits); "spawn_delay_ticks"
  * = fault injection: each background job sleeps that long (default 0) once it
- * has marked a record DRAWING, so resets meet jobs in flight. Results are the
- * same for any values. Returns SNAKE_E_ARG for an unknown name or a value out of
+ * has marked a record DRAWING, so resets meet jobs in flight; "fused" = 1 runs
+ * the step as one launch (k_step) where the configuration allows it (one
+ * frame, at most 4 snakes, table encode, in-step spawn-ahead; default 0);
+ * "fuse_roles" = which of k_step's roles run (diagnostics; 7 = all). Results
+ * are the same for any values of the first three. Returns SNAKE_E_ARG for an unknown name or a value out of
  * range. */
 int snake_debug_set(const char *name, long long value);
 

@@ -338,6 +338,19 @@ static int64_t queue_cap(int64_t N, int64_t E)
     return (blocks + kQShards - 1) / kQShards * E;
 }
 
+// The fused step's area of resetq (snake_kernels.hip k_step), after the two
+// queue sets: 64 logic-done counts (one line each), the groups' done and claim
+// flags (at most N / 4 groups), the encodes' hand-off records (uint4 per env).
+int64_t fused_base(int64_t N)
+{
+    const int64_t cap = std::max(queue_cap(N, 4), std::max(queue_cap(N, 8), queue_cap(N, 16)));
+    return round_up(kQSets * (kNumQ * kQShards * cap + kQCounters), 4);
+}
+int64_t fused_words(int64_t N)
+{
+    return kQShards * kQSpread + 2 * round_up((N + 3) / 4, 4) + 4 * N;
+}
+
 int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
 {
     int rc = check_cfg(c);
@@ -377,8 +390,8 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
         // kQShards) with room for every env of its blocks, + the step's counters
         // (kQCount, each in its own line); sized for any k_logic lane grouping
-        const int64_t cap = std::max(queue_cap(N, 4), std::max(queue_cap(N, 8), queue_cap(N, 16)));
-        o->resetq = kQSets * (kNumQ * kQShards * cap + kQCounters) * 4;
+        // + the fused step's flags, counts and hand-off records
+        o->resetq = (fused_base(N) + fused_words(N)) * 4;
     }
     o->obs = N * S * oh * ow * 8 * fs;
     o->rew = N * S * 8;
@@ -574,6 +587,20 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     if (k->lds_bytes > 64 * 1024) {
         set_error("grid ring of %d bytes per env does not fit the LDS budget", k->ring_bytes);
         return SNAKE_E_CONFIG;
+    }
+    {   // the fused step (snake_kernels.hip k_step): all-done auto-reset in the step
+        // with the one-wave table encode (4 envs per wave), one frame and at most
+        // 4 snakes (the hand-off record's crop centres), in-step spawn-ahead
+        const int E = kWave / k->logic_ms;
+        k->nlg = (int)((N + E - 1) / E);
+        k->fused = c->autoreset == 1 && k->tbl && !k->lean && !k->bg && k->fs == 1 && k->S <= 4 &&
+                   k->enc_per_wave == 4 && E % 4 == 0 && (k->link32 || k->link_in_lds) ? 1 : 0;
+        const int64_t fb = fused_base(N), groups = round_up((N + 3) / 4, 4);
+        k->fu_ldone = fb;
+        k->fu_done = fb + kQShards * kQSpread;
+        k->fu_claim = k->fu_done + groups;
+        k->fu_hoff = k->fu_claim + groups;
+        k->epoch = 0;
     }
     k->rf = c->rew_fruit; k->rk = c->rew_kill; k->rl = c->rew_lose; k->rw = c->rew_win;
     k->rt = c->rew_time; k->max_steps = c->max_episode_steps;

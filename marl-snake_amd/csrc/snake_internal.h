@@ -110,11 +110,20 @@ struct KCfg {
     // unit descriptors
     int tbl, tbl_base, tbl_pat, tbl_desc, lds_tbl_bytes;
     uint32_t mag_ups, mag_rowl, mag_fs, mag_wpr;
+    // fused step (k_step, snake_kernels.hip): on, the logic groups, the step's
+    // epoch, and word offsets into resetq of the logic-done counts, the groups'
+    // done and claim flags, and the encodes' hand-off records (uint4 per env)
+    int fused, nlg, fu_roles;
+    uint32_t epoch;
+    int64_t fu_ldone, fu_done, fu_claim, fu_hoff;
     double rf, rk, rl, rw, rt, max_steps;
 };
 
 int build_kcfg(const snake_cfg *c, int64_t num_envs, int64_t n_cand, KCfg *k);
 int layout_of(const snake_cfg *c, int64_t num_envs, snake_layout *out);
+// word offset in resetq of the fused step's area (after the two queue sets), and its words
+int64_t fused_base(int64_t num_envs);
+int64_t fused_words(int64_t num_envs);
 void set_error(const char *fmt, ...);
 
 // launchers (snake_kernels.hip)

@@ -68,6 +68,16 @@ __device__ unsigned long long g_gate_shut[kDiagSlots * kDiagSpread];    // k_log
 __device__ unsigned long long g_draw_wait[kDiagSlots * kDiagSpread];    // resets that waited for a background job (DRAWING)
 __device__ unsigned long long g_draw_timeout[kDiagSlots * kDiagSpread]; // ... and gave up waiting (drew from the env's own state)
 #define DIAG_ADD(arr) atomicAdd(&(arr)[(blockIdx.x % kDiagSlots) * kDiagSpread], 1ull)
+#ifdef SNAKE_FUSE_DEBUG
+// (diagnostic build: range checks on the fused step's indices; a violation is
+// recorded -- site, value -- and the access skipped)
+__device__ unsigned long long g_fdbg[64];
+#define FDBG_BAD(site, val) (atomicAdd(&g_fdbg[2 * (site)], 1ull), atomicMax(&g_fdbg[2 * (site) + 1], (unsigned long long)(uint32_t)(val)), true)
+#define FDBG_MARK(site) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_fdbg[2 * (site)], 1ull); } while (0)
+#else
+#define FDBG_BAD(site, val) false
+#define FDBG_MARK(site) do {} while (0)
+#endif
 
 #ifdef SNAKE_STAMPS
 // Diagnostic build only (scripts/logic_stamps.py): s_memtime stamps of block
@@ -315,6 +325,31 @@ __device__ __forceinline__ void obs_store(T *p, const T &v)
 }
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+// The 128-byte lines an env's observation shares with its neighbours (an env of
+// 3 872 bytes, cfg3/cfg4, starts 32 bytes into a line in three of four envs):
+// byte offsets [0, lf) and [hf, bytes) of the env's observation at obs_env.
+// Those chunks are stored write-back (obs_store_edge), so the L2 merges the two
+// envs' parts of the line; as non-temporal stores each part went to memory on
+// its own. Round 6, scripts/microbench/storebw2.hip ENV_PATTERN (254 MB, four
+// 3 872-byte envs per wave, env by env): non-temporal 4.49 TB/s, write-back
+// 5.33, non-temporal with aligned 1 KB instructions 5.23.
+#ifndef SNAKE_OBS_EDGE_WB
+#define SNAKE_OBS_EDGE_WB 1
+#endif
+__device__ __forceinline__ void obs_edges(const uint8_t *obs_env, int bytes, int &lf, int &hf)
+{
+    const uint32_t lo = (uint32_t)(uintptr_t)obs_env;
+    lf = SNAKE_OBS_EDGE_WB ? (int)((0u - lo) & 127u) : 0;
+    hf = SNAKE_OBS_EDGE_WB ? bytes - (int)((lo + (uint32_t)bytes) & 127u) : bytes;
+}
+// (x: the chunk's byte offset in the env's observation)
+template <typename T>
+__device__ __forceinline__ void obs_store_edge(T *p, const T &v, int x, int lf, int hf)
+{
+    if (x < lf || x >= hf) *p = v;
+    else obs_store(p, v);
+}
 
 constexpr int kRespawnT = 4;   // raws per lane prefetched by the fast fruit respawn
 
@@ -817,6 +852,8 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
     int i = rest % c.oh;
     int k = rest / c.oh;
     const bool wide = (U & 1) == 0;
+    int lf, hf;
+    obs_edges(obs_env, 8 * U, lf, hf);
     for (int p = lane; p < pairs; p += kWave) {
         int s = slot0 + f;
         s -= (s >= fs) ? fs : 0;
@@ -834,7 +871,7 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
             uint4 v;
             v.x = (uint32_t)a; v.y = (uint32_t)(a >> 32);
             v.z = (uint32_t)b; v.w = (uint32_t)(b >> 32);
-            obs_store(reinterpret_cast<v4u *>(obs_env + 16 * (int64_t)p), (v4u){v.x, v.y, v.z, v.w});
+            obs_store_edge(reinterpret_cast<v4u *>(obs_env + 16 * (int64_t)p), (v4u){v.x, v.y, v.z, v.w}, 16 * p, lf, hf);
         } else {
             obs_store(reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p), a);
             if (has_b) obs_store(reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p + 8), b);
@@ -1071,12 +1108,33 @@ __device__ __forceinline__ uint32_t *spawn_rec(const KCfg &c, const snake_state 
 // record with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility).
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p)
 {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load((const gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v)
 {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 8-byte forms (global address space: never flat), and 16 bytes as two of them
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ unsigned long long ld_sc1_64(const void *p)
+{
+    return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_64(void *p, unsigned long long v)
+{
+    __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_128(void *p, uint4 v)
+{
+    st_sc1_64(p, (unsigned long long)v.x | ((unsigned long long)v.y << 32));
+    st_sc1_64((uint8_t *)p + 8, (unsigned long long)v.z | ((unsigned long long)v.w << 32));
+}
+__device__ __forceinline__ uint4 ld_sc1_128(const void *p)
+{
+    const unsigned long long a = ld_sc1_64(p), b = ld_sc1_64((const uint8_t *)p + 8);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+
 __device__ __forceinline__ void mt_load_sc1(WaveMT &m, const uint32_t *g, int pos, int lane)
 {
 #pragma unroll
@@ -1345,7 +1403,12 @@ __device__ __forceinline__ void logic_load(const int blk, LogicIn &in)
     }
 }
 
-template <int MS, bool BG>
+// FU: the fused step (k_step): the stores another wave of the same launch reads
+// or writes are write-through (sc1) and drained before the group's done flag
+// and the logic-done counter; an env whose episode ended stores nothing its
+// auto-reset rewrites (records, statistics, ring words, crop centres, frame):
+// the two would race in two XCDs' L2s (k_step, below).
+template <int MS, bool BG, bool FU = false>
 __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
 {
     LSTAMP(40);
@@ -1616,9 +1679,10 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
         hbuf = (hbuf & ~(3 << (2 * ho))) | (dir << (2 * ho));
         const int hfull = hbuf;                                      // the head word's directions
         if (ho == 0) {                                               // the head word is complete
-            *reinterpret_cast<uint32_t *>(ring + rh) = (uint32_t)(hbuf & 3) | ((uint32_t)(hbuf >> 2 & 3) << 8) |
-                                                       ((uint32_t)(hbuf >> 4 & 3) << 16) |
-                                                       ((uint32_t)(hbuf >> 6 & 3) << 24);
+            if (!FU || !ep_end)
+                *reinterpret_cast<uint32_t *>(ring + rh) = (uint32_t)(hbuf & 3) | ((uint32_t)(hbuf >> 2 & 3) << 8) |
+                                                           ((uint32_t)(hbuf >> 4 & 3) << 16) |
+                                                           ((uint32_t)(hbuf >> 6 & 3) << 24);
             hbuf = 0;
         }
         if (!eat) {                                                  // directions.pop()
@@ -1802,7 +1866,13 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
         WaveMT mt;
         mt_load(mt, st.mt + ee * kMtN, bcast(mtpos, L), lane);
         place_fruits(c, lds + gg * stride, mt, bcast(fruit_taken, L), fbuf, lane);
-        mt_store(mt, st.mt + ee * kMtN, lane);
+        if constexpr (FU) {   // (a reset or spawn-ahead job of this launch may read the key)
+#pragma unroll
+            for (int t = 0; t < 10; t++)
+                if (64 * t + lane < kMtN) st_sc1(st.mt + ee * kMtN + 64 * t + lane, mt.w[t]);
+        } else {
+            mt_store(mt, st.mt + ee * kMtN, lane);
+        }
         if (g == gg) { mtpos_new = mt.pos; mt_slow = true; }
     }
     // a draw from the MT state voids the env's spawn-ahead record
@@ -1834,20 +1904,33 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     LSTAMP(48);
     if (qm) {            // queue the auto-resets in the slots claimed above
         const int base = bcast(qbase, 0);
-        if ((qm >> lane) & 1ull) qb[shard * c.q_cap + base + mbcnt64(qm)] = e;
+        if ((qm >> lane) & 1ull) {
+            int *qp = qb + shard * c.q_cap + base + mbcnt64(qm);
+            if constexpr (FU) st_sc1(reinterpret_cast<uint32_t *>(qp), (uint32_t)e);
+            else *qp = e;
+        }
     }
     // and the spawn-ahead jobs (background: with the generation they were queued at)
     const int pent = BG ? (int)((uint32_t)e | ((spw1 >> 3) << (32 - kQGenBits))) : e;
     if (pm) {
         const int base = bcast(pbase, 0);
-        if ((pm >> lane) & 1ull) qb[(kQShards + shard) * c.q_cap + base + mbcnt64(pm)] = pent;
+        if ((pm >> lane) & 1ull) {
+            int *qp = qb + (kQShards + shard) * c.q_cap + base + mbcnt64(pm);
+            if constexpr (FU) st_sc1(reinterpret_cast<uint32_t *>(qp), (uint32_t)pent);
+            else *qp = pent;
+        }
     }
     if (pn) {
         const int base = bcast(nbase, 0);
-        if ((pn >> lane) & 1ull) qb[(2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn)] = pent;
+        if ((pn >> lane) & 1ull) {
+            int *qp = qb + (2 * kQShards + shard) * c.q_cap + base + mbcnt64(pn);
+            if constexpr (FU) st_sc1(reinterpret_cast<uint32_t *>(qp), (uint32_t)pent);
+            else *qp = pent;
+        }
     }
     if (env_ok && k == 0 && !bad && spw_wr) {
         if (BG) atomicExch(reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN), spw1);
+        else if (FU) st_sc1(reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN), spw1);
         else st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)spw1;
     }
     LSTAMP(49);
@@ -1863,7 +1946,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     if (ep_end) { s0 = 0.0; s1 = s2 = s3 = 0u; }                   // _reset_epi_stats
     // a snake dead before this step keeps its statistics, record and (one frame)
     // crop centre: no stores for it
-    if (live && (counted || ep_end)) {
+    if (live && (counted || ep_end) && !(FU && ep_end)) {
         const unsigned long long sb = (unsigned long long)__double_as_longlong(s0);
         *sp = make_uint4((uint32_t)sb, (uint32_t)(sb >> 32), s1, (s2 & 0xffffu) | (s3 << 16));
     }
@@ -1877,9 +1960,12 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
             const int q = q0 + lane, gg = min(fdiv((uint32_t)q, c.mag_n16, n16), E - 1);
             const int off = q - gg * n16;
             const int ng = __shfl(ncur, gg * G);
-            const int bg = __shfl((int)bad, gg * G);
-            if (q < E * n16 && e0 + gg < c.N && !bg)
-                dst[((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)ng * stride) / 16 + off] = s4[q];
+            const int bg = __shfl((int)(bad || (FU && ep_end)), gg * G);
+            if (q < E * n16 && e0 + gg < c.N && !bg) {
+                uint4 *d = dst + ((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)ng * stride) / 16 + off;
+                if constexpr (FU) st_sc1_128(d, s4[q]);   // (the encodes read it in this launch)
+                else *d = s4[q];
+            }
         }
     }
     // crop centre = the own HEAD cell: the new head while alive, (0,0) when dead
@@ -1887,16 +1973,43 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     if (env_ok && k == 0 && !bad) {
         int4 ner;
         ner.x = alive_snakes; ner.y = eplen1; ner.z = ncur; ner.w = mtpos_new;
-        *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = ner;
+        // (FU: this env's auto-reset in this launch reads the MT position)
+        if constexpr (FU) st_sc1_128(st.env + (int64_t)e * kEnvRec, make_uint4(ner.x, ner.y, ner.z, ner.w));
+        else *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = ner;
     }
-    if (live && (counted || fs > 1)) st.ctr[((int64_t)e * fs + ncur) * S + k] = (uint16_t)((chr << 8) | chc);
-    if (live && counted) {
+    if (live && (counted || fs > 1) && !(FU && ep_end)) st.ctr[((int64_t)e * fs + ncur) * S + k] = (uint16_t)((chr << 8) | chc);
+    if constexpr (FU) {
+        // the encodes' hand-off record of env e (k_step): the slot to encode,
+        // whether the env auto-resets (its reset writes the observation), the S
+        // <= 4 crop centres (the own head, (0,0) when dead; an env rejected for
+        // an invalid action keeps its slot and heads)
+        const int aw = bad ? (isn && ((rec.y >> 8) & 1)) : alive;
+        const int cv2 = aw ? (bad ? (hr << 8) | hc : (chr << 8) | chc) : 0;
+        const int c0 = gsel<G, 0>(cv2), c1 = gsel<G, 1>(cv2), c2 = gsel<G, 2>(cv2), c3 = gsel<G, 3>(cv2);
+        if (env_ok && k == 0) {
+            const uint32_t slot = bad ? (uint32_t)cur : (uint32_t)ncur;
+            st_sc1_128(st.resetq + c.fu_hoff + 4 * (int64_t)e,
+                       make_uint4(slot | ((ep_end && !bad) ? 256u : 0u), (uint32_t)(c0 & 0xffff) | ((uint32_t)c1 << 16),
+                                  (uint32_t)(c2 & 0xffff) | ((uint32_t)c3 << 16), 0u));
+        }
+    }
+    if (live && counted && !(FU && ep_end)) {
         int4 nrec;
         nrec.x = nhr | (nhc << 8) | (ntr << 16) | (ntc << 24);
         nrec.y = dir | (alive << 8) | (hbuf << 16);
         nrec.z = rh | (rl << 16);
         nrec.w = (int)tq;                 // entry 0 = the new directions[-1]
         reinterpret_cast<int4 *>(st.snake)[(int64_t)e * S + k] = nrec;
+    }
+    if constexpr (FU) {
+        // publish (MI355X_MICROARCH.md, inter-workgroup visibility, R1): every
+        // write-through store drained, then the group's done flag (encodes) and
+        // the sharded logic-done count (reset workers)
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            st_sc1(reinterpret_cast<uint32_t *>(st.resetq + c.fu_done) + blk, c.epoch);
+            atomicAdd(reinterpret_cast<unsigned *>(st.resetq + c.fu_ldone) + (blk % kQShards) * kQSpread, 1u);
+        }
     }
     LSTAMP(47);
 }
@@ -2136,6 +2249,9 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
         if (idx < R) {
             __builtin_amdgcn_s_setprio(3);
             const int e = job_env(0, idx, incl);
+#ifdef SNAKE_FUSE_DEBUG
+            if ((e < 0 || e >= J.c.N) && FDBG_BAD(1, e)) { idx = 1 << 30; break; }
+#endif
             ITEM_T0();
             WaveMT mt;
             uint32_t cellw;
@@ -2152,6 +2268,9 @@ __device__ __forceinline__ void autoreset_worker(const int wid, const int G, uin
             else __builtin_amdgcn_s_setprio(3);
             const int j = idx - R;
             const int e = j < U ? job_env(1, j, uincl) : job_env(2, j - U, nincl);
+#ifdef SNAKE_FUSE_DEBUG
+            if ((e < 0 || e >= J.c.N) && FDBG_BAD(2, e)) { idx = 1 << 30; break; }
+#endif
             if (J.c.diag && lane == 0) DIAG_ADD(g_spawn_jobs);
             ITEM_T0();
             do_spawn<MS, JL>(J.c, J.st, e, lds, wid, lane);
@@ -2363,7 +2482,10 @@ __device__ __forceinline__ void tsync()
     else __syncthreads();
 }
 
-template <int NPW, int T = kWave>
+// FU (k_step): the frames and the hand-off record (slot, reset flag, crop
+// centres) of the logic wave that finished these envs in this launch, all read
+// with write-through-coherent (sc1) loads after its done flag
+template <int NPW, int T = kWave, bool FU = false>
 __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const snake_out &o, const int blk)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -2411,10 +2533,18 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
     do {                                                                                           \
         const int64_t e_ = (EE);                                                                   \
         const uint32_t *r32_ = reinterpret_cast<const uint32_t *>(st.grid + e_ * c.ring_bytes);    \
-        _Pragma("unroll") for (int u = 0; u < NPW; u++) w[u] = r32_[src[u]];                       \
-        pcur = st.env[e_ * kEnvRec + ENV_CUR];                                                     \
-        pctr = lane < fsS ? st.ctr[e_ * fsS + lane] : 0;                                           \
-        pskip = c.autoreset ? o.ep_done[e_] : 0;                                                   \
+        if constexpr (FU) {                                                                        \
+            _Pragma("unroll") for (int u = 0; u < NPW; u++) w[u] = ld_sc1(r32_ + src[u]);          \
+            const uint4 h_ = ld_sc1_128(st.resetq + c.fu_hoff + 4 * e_);                           \
+            pcur = (int)(h_.x & 255u);                                                             \
+            pskip = (int)((h_.x >> 8) & 1u);                                                       \
+            pctr = lane < fsS ? (int)(((lane < 2 ? h_.y : h_.z) >> (16 * (lane & 1))) & 0xffffu) : 0; \
+        } else {                                                                                   \
+            _Pragma("unroll") for (int u = 0; u < NPW; u++) w[u] = r32_[src[u]];                   \
+            pcur = st.env[e_ * kEnvRec + ENV_CUR];                                                 \
+            pctr = lane < fsS ? st.ctr[e_ * fsS + lane] : 0;                                       \
+            pskip = c.autoreset ? o.ep_done[e_] : 0;                                               \
+        }                                                                                          \
     } while (0)
     if (e_begin < e_end) SNAKE_TBL_FETCH(e_begin);
     const int chunks = c.units >> 1;
@@ -2446,6 +2576,8 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
         if (!skip) {
             tsync<T>();
             v4u *out = reinterpret_cast<v4u *>(o.obs + (int64_t)e * c.units * 8);
+            int lf, hf;
+            obs_edges(o.obs + (int64_t)e * c.units * 8, c.units * 8, lf, hf);
             auto lookup = [&](uint2 dd) {   // units 2q, 2q + 1 of descriptor pair dd
                 const uint2 b0 = base[dd.x >> 16], b1 = base[dd.y >> 16];
                 const uint32_t v0 = pf[b0.x + (dd.x & 0xffffu)], v1 = pf[b1.x + (dd.y & 0xffffu)];
@@ -2459,7 +2591,7 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
                 for (int t = 0; t < 4; t++) r[t] = lookup(dr[t]);
 #pragma unroll
                 for (int t = 0; t < 4; t++)
-                    if (t * T + lane < chunks) obs_store(out + t * T + lane, r[t]);
+                    if (t * T + lane < chunks) obs_store_edge(out + t * T + lane, r[t], 16 * (t * T + lane), lf, hf);
             } else {
             // CP chunks per lane and pass, their lookup chains interleaved
             // (clamped reads; only the chunks that exist are stored); two in
@@ -2472,12 +2604,167 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
                     r[t] = lookup(reinterpret_cast<const uint2 *>(desc)[min(q0 + t * T + lane, chunks - 1)]);
 #pragma unroll
                 for (int t = 0; t < CP; t++)
-                    if (q0 + t * T + lane < chunks) obs_store(out + q0 + t * T + lane, r[t]);
+                    if (q0 + t * T + lane < chunks)
+                        obs_store_edge(out + q0 + t * T + lane, r[t], 16 * (q0 + t * T + lane), lf, hf);
             }
             }
         }
     }
 #undef SNAKE_TBL_FETCH
+}
+
+// ------------------------------------------------------------ fused step
+// k_step (round 6): the whole step as ONE launch on boards whose encodes take
+// the table form in one wave and whose hand-off record holds the crop centres
+// (one frame, S <= 4: cfg2, cfg3, cfg4), no background spawn kernel. Blocks
+// [0, nlg) are k_logic's env groups, the next reset_slots blocks the reset
+// workers, the rest the table encodes (4 envs each). The encodes of a group
+// start as soon as that group's rules are done instead of after the last
+// group and a kernel boundary, so k_logic's latency chain runs beside the
+// encodes' stores.
+// Dispatch order, timing and placement are not assumed (MI355X_MICROARCH.md
+// "Workgroup dispatch", contract [G]): every logic group is CLAIMED (an atomic
+// exchange of the step's epoch) by whichever wave gets it first -- its own
+// block, or an encode block of that group that finds it unclaimed, or a reset
+// worker that has waited long -- and the claimer runs it at once without
+// waiting on anything. A wave waits only for a group that is claimed, i.e.
+// running, so the launch cannot deadlock.
+// Hand-offs (R1 of the guide's visibility rules): the logic wave's stores that
+// another wave of the launch reads or writes are write-through (sc1) stores --
+// the new frame, the env record, the queue entries, the spawn status word, a
+// rewritten MT key, the encodes' hand-off record -- drained (vmcnt(0)) before
+// the group's done flag (sc1 store of the epoch) and its logic-done count (an
+// atomic add on shard blk % 64); an env whose episode ended stores nothing its
+// auto-reset rewrites. The encodes poll the flag and read their inputs with sc1
+// loads only; the workers poll the 64 counts, then one agent-scope acquire,
+// then the queues and env state as before. Epochs: the library's per-state step
+// count (launch_step); the counts grow by their shard's group count per step.
+// Every wait is bounded (kFuseWait): past it the wave carries on and the launch
+// counts the timeout ("fused_timeout"), the results are then undefined.
+__device__ unsigned long long g_fused_timeout[kDiagSlots * kDiagSpread];
+constexpr unsigned long long kFuseWait = 10000000ull;   // 100 ms of the 100 MHz clock
+constexpr unsigned long long kFuseHelp = 2000ull;       // 20 us: a waiting worker then claims unclaimed groups
+
+// (Everything here is inlined into k_step: kargs() reads the kernarg segment
+// pointer, which a called function does not have -- an out-of-line
+// fused_logic read its KCfg from garbage and faulted, round 6.)
+__device__ __forceinline__ bool fused_claim(const int g)
+{
+    const KCfg &c = kargs().c;
+    uint32_t *claim = reinterpret_cast<uint32_t *>(kargs().st.resetq + c.fu_claim) + g;
+    int won = 0;
+    if ((threadIdx.x & (kWave - 1)) == 0) won = atomicExch(claim, c.epoch) != c.epoch ? 1 : 0;
+    return __shfl(won, 0) != 0;
+}
+
+__device__ __forceinline__ bool fused_group_done(const int g)
+{
+    const KCfg &c = kargs().c;
+    const uint32_t *done = reinterpret_cast<const uint32_t *>(kargs().st.resetq + c.fu_done) + g;
+    return (uint32_t)__shfl((int)ld_sc1(done), 0) == c.epoch;
+}
+
+// an encode block's wait for its group's rules, which some wave has claimed
+__device__ __forceinline__ void fused_wait_group(const int g)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (!fused_group_done(g)) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kFuseWait) {
+            if ((threadIdx.x & (kWave - 1)) == 0) DIAG_ADD(g_fused_timeout);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+// A reset worker's wait for every group's rules (the queues complete): -1 once
+// they are done (or the wait timed out), else a group it has just claimed and
+// must run -- once it has waited kFuseHelp, every group still unclaimed, from a
+// worker-specific start (`scan`: the next scan position, -1 before the first)
+__device__ __forceinline__ int fused_wait_all(const int wid, const unsigned long long t0, int &scan)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    for (;;) {
+        const KCfg &c = kargs().c;
+        const int nlg = c.nlg;
+        // shard s (lane s) counts the groups g = s mod 64: (nlg - s + 63) / 64 of them per step
+        const uint32_t ns = lane < nlg ? (uint32_t)((nlg - lane + kQShards - 1) / kQShards) : 0u;
+        const uint32_t v = ld_sc1(reinterpret_cast<const uint32_t *>(kargs().st.resetq + c.fu_ldone) + lane * kQSpread);
+        if (__ballot(v != c.epoch * ns) == 0ull) return -1;
+        const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+        if (dt > kFuseWait) {
+            if (lane == 0) DIAG_ADD(g_fused_timeout);
+            return -1;
+        }
+        if (dt > kFuseHelp && scan < nlg) {
+            if (scan < 0) scan = 0;
+            for (; scan < nlg; scan += kWave) {
+                const int g = (wid * 61 + scan + lane) % nlg;
+                const KCfg &c2 = kargs().c;
+                const uint32_t cl = scan + lane < nlg ? ld_sc1(reinterpret_cast<const uint32_t *>(kargs().st.resetq + c2.fu_claim) + g)
+                                                      : c2.epoch;
+                unsigned long long m = __ballot(cl != c2.epoch);
+                while (m) {
+                    const int L = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    const int gg = __shfl(g, L);
+                    if (fused_claim(gg)) return gg;   // (the next call rescans this pass)
+                }
+            }
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+// (four waves per SIMD: at most 128 VGPRs; the rules alone take 100, the
+// worker path in k_post 71)
+template <int MS, int NPW, int JL>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_step(const KArgs)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    PTIME(0);
+    const int b = (int)blockIdx.x;
+    const int nlg = kargs().c.nlg, G = kargs().c.reset_slots;
+    const int roles = kargs().c.fu_roles;   // (snake_debug_set "fuse_roles": 7 = all)
+    const int role = b < nlg ? 0 : (b < nlg + G ? 1 : 2);   // rules, reset worker, encodes
+    if (!(roles & (1 << role))) return;
+    const int j = b - nlg - G;   // (encodes: envs 4j .. 4j + 3, all of logic group 4j / (64 / MS))
+    const int eg = (4 * j) / (kWave / MS);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int scan = -1;
+    // the rules of every group this wave claims, at ONE inlined site
+    for (int it = 0;; it++) {
+        int grp = -1;
+        if (role == 0) {
+            if (it == 0 && fused_claim(b)) grp = b;
+        } else if (role == 2) {
+            if (it == 0 && !fused_group_done(eg) && fused_claim(eg)) grp = eg;
+        } else {
+            grp = fused_wait_all(b - nlg, t0, scan);
+        }
+        if (grp < 0) break;
+        LogicIn in;
+        logic_load<MS, false>(grp, in);
+        logic_body<MS, false, true>(grp, in);
+        FDBG_MARK(3);
+    }
+    if (role == 0) { PTIME(1); return; }
+    if (role == 1) {
+        // the queues, env records, MT keys and spawn records the groups published
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        FDBG_MARK(4);
+        autoreset_worker<4, false, JL>(b - nlg, G, lds);
+        FDBG_MARK(5);
+        PTIME(1);
+        return;
+    }
+    if (4 * j >= kargs().c.N && FDBG_BAD(6, j)) return;
+    fused_wait_group(eg);
+    FDBG_MARK(7);
+    const KArgs &A = kargs();
+    encode_tbl_block<NPW, kWave, true>(A.c, A.st, A.o, j);
+    PTIME(1);
 }
 
 // NPF > 0: encode_multi<NPF>; 0: encode_one; -NPW: encode_tbl_block<NPW>
@@ -2693,6 +2980,11 @@ std::mutex g_tmu;
 bool g_timing = false;
 int g_draw_wait_ticks = 200000;   // KCfg.draw_wait (snake_debug_set "draw_wait_ticks")
 int g_spawn_delay_ticks = 0;      // KCfg.spawn_delay (snake_debug_set "spawn_delay_ticks")
+int g_fuse_roles = 7;             // KCfg.fu_roles (snake_debug_set "fuse_roles", diagnostics)
+#ifndef SNAKE_FUSED
+#define SNAKE_FUSED 0
+#endif
+int g_fused = SNAKE_FUSED;        // the fused step where KCfg.fused allows it (snake_debug_set "fused")
 std::vector<TimingRec> g_pending;
 std::vector<hipEvent_t> g_pool;
 std::map<std::string, std::pair<double, int64_t>> g_done;
@@ -2808,6 +3100,9 @@ struct BgCtx {
 };
 static std::mutex g_bgmu;
 static std::map<const void *, BgCtx> g_bg;
+// The fused step's per-state epoch (k_step): the number of k_step launches of
+// the state so far; its flag area is zeroed on the state's first fused step.
+static std::map<const void *, uint32_t> g_fu;
 
 static void destroy_bg(BgCtx &c)
 {
@@ -2862,6 +3157,7 @@ int release_background(const snake_state &st)
     BgCtx c;
     {
         std::lock_guard<std::mutex> g(g_bgmu);
+        g_fu.erase(st.env);
         auto it = g_bg.find(st.env);
         if (it == g_bg.end()) return SNAKE_OK;
         c = it->second;
@@ -2973,6 +3269,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
     k.diag = g_timing ? 1 : 0;
     k.draw_wait = g_draw_wait_ticks;
     k.spawn_delay = g_spawn_delay_ticks;
+    k.fu_roles = g_fuse_roles;
     const hipStream_t sm = (hipStream_t)stream;
     DeviceGuard dg(sm);
     if (dg.dev < 0) return SNAKE_E_LAUNCH;
@@ -2988,6 +3285,41 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         if (!(bgc = bg_ctx(st, true))) return SNAKE_E_LAUNCH;
         k.qpar = (int)(bgc->steps & 1);
         k.spawn_gate = bgc->launched[k.qpar];
+    }
+    if (k.fused && g_fused) {   // the whole step as one launch (k_step)
+        uint32_t ep;
+        bool fresh = false;
+        {
+            std::lock_guard<std::mutex> g(g_bgmu);
+            auto it = g_fu.find(st.env);
+            if (it == g_fu.end()) { it = g_fu.emplace(st.env, 0u).first; fresh = true; }
+            ep = it->second;
+        }
+        if (fresh && hipMemsetAsync(st.resetq + k.fu_ldone, 0, sizeof(int) * fused_words(k.N), sm) != hipSuccess) {
+            set_error("zeroing the fused step's flags failed");
+            return SNAKE_E_LAUNCH;
+        }
+        k.epoch = ep + 1;
+        const int npw = (k.fs * k.HW / 4 + kWave - 1) / kWave;
+        const dim3 gf(k.nlg + k.reset_slots + (k.N + 3) / 4), bf(kWave);
+        const int lds_f = std::max(k.lds_logic, std::max(k.lds_bytes, k.lds_tbl_bytes));
+        const KArgs fa{k, st, o, actions};
+        TimedLaunch tf("k_step", sm);
+        auto go = [&](auto msc, auto npwc) {
+            constexpr int MS = decltype(msc)::value, NPW = decltype(npwc)::value;
+            if (k.link32) slaunch((k_step<MS, NPW, 2>), gf, bf, lds_f, sm, fa);
+            else slaunch((k_step<MS, NPW, 1>), gf, bf, lds_f, sm, fa);
+        };
+        using I2 = std::integral_constant<int, 2>;
+        using I4 = std::integral_constant<int, 4>;
+        using I8 = std::integral_constant<int, 8>;
+        if (ms == 4) { if (npw <= 2) go(I4{}, I2{}); else go(I4{}, I8{}); }
+        else { if (npw <= 2) go(I8{}, I2{}); else go(I8{}, I8{}); }
+        tf.close();
+        if (int rc2 = check_launch("k_step")) return rc2;
+        std::lock_guard<std::mutex> g(g_bgmu);
+        g_fu[st.env] = ep + 1;
+        return SNAKE_OK;
     }
     TimedLaunch t1("k_logic", sm);
     // Background spawn-ahead: the fork onto the background stream is k_logic's
@@ -3167,12 +3499,21 @@ extern "C" int snake_timing_enable(int on)
     return SNAKE_OK;
 }
 
+#ifdef SNAKE_FUSE_DEBUG
+extern "C" int snake_debug_fdbg(unsigned long long *out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(snake::g_fdbg), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int snake_debug_set(const char *name, long long value)
 {
     if (name && value >= 0 && value <= INT_MAX) {
         std::lock_guard<std::mutex> g(snake::g_tmu);
         if (!strcmp(name, "draw_wait_ticks")) { snake::g_draw_wait_ticks = (int)value; return SNAKE_OK; }
         if (!strcmp(name, "spawn_delay_ticks")) { snake::g_spawn_delay_ticks = (int)value; return SNAKE_OK; }
+        if (!strcmp(name, "fuse_roles")) { snake::g_fuse_roles = (int)value; return SNAKE_OK; }
+        if (!strcmp(name, "fused")) { snake::g_fused = value ? 1 : 0; return SNAKE_OK; }
     }
     snake::set_error("snake_debug_set: unknown knob or value out of range");
     return SNAKE_E_ARG;
@@ -3195,7 +3536,8 @@ extern "C" int snake_timing_read(const char *kernel, double *total_ms, int64_t *
                     : !strcmp(kernel, "respawn_slow2") ? (const void *)snake::g_resp_slow2
                     : !strcmp(kernel, "gate_shut") ? (const void *)snake::g_gate_shut
                     : !strcmp(kernel, "draw_wait") ? (const void *)snake::g_draw_wait
-                    : !strcmp(kernel, "draw_timeout") ? (const void *)snake::g_draw_timeout : nullptr;
+                    : !strcmp(kernel, "draw_timeout") ? (const void *)snake::g_draw_timeout
+                    : !strcmp(kernel, "fused_timeout") ? (const void *)snake::g_fused_timeout : nullptr;
     if (sym) {
         const int n = one ? 1 : snake::kDiagSlots * snake::kDiagSpread;
         std::vector<unsigned long long> v(n, 0ull), z(n, 0ull);

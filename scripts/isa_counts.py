@@ -20,7 +20,7 @@ FLAGS = ['-O3', '-std=c++17', '-ffp-contract=off', '--offload-arch=gfx950', '-ml
 
 
 def demangle(name):
-    r = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-cxxfilt', name], capture_output=True, text=True)
+    r = subprocess.run(['c++filt', name], capture_output=True, text=True)
     return r.stdout.strip().replace('snake::', '') or name
 
 

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
@@ -53,6 +54,45 @@ __global__ void k_seg(uint8_t *out, const uint8_t *in, int64_t total, int seg, i
     }
     const int n = seg / W;
     for (int c = lane; c < n; c += 64) st<W, POL>(out + base + (int64_t)c * W, (uint32_t)c + acc);
+}
+
+// Each wave writes K sub-segments of SUB bytes: sub-segment k of wave w at
+// (k * NW + w) * SUB (interleaved over the buffer), or at (w * K + k) * SUB
+// (contiguous) -- k_seg with seg = K * SUB.
+template <int W, int POL>
+__global__ void k_sub(uint8_t *out, int64_t nw, int sub, int K)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wave >= nw) return;
+    const int n = sub / W;
+    for (int k = 0; k < K; k++) {
+        uint8_t *o = out + ((int64_t)k * nw + wave) * sub;
+        for (int c = lane; c < n; c += 64) st<W, POL>(o + (int64_t)c * W, (uint32_t)c);
+    }
+}
+
+// The encode's store pattern: every wave writes K consecutive envs of ENV
+// bytes (K * ENV contiguous), either env by env (chunk t * 64 + lane of each
+// env: instructions start at the env's offset, partial lines at the env
+// boundaries) or as aligned 1 KB instructions over the K-env region.
+template <int POL, bool REGION>
+__global__ void k_envs(uint8_t *out, int n_env, int env_bytes, int K)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t e0 = wave * K;
+    if (e0 >= n_env) return;
+    const int ke = (int)min((int64_t)K, n_env - e0);
+    const int cpe = env_bytes / 16;
+    uint8_t *o = out + e0 * env_bytes;
+    if (REGION) {
+        const int n = ke * cpe;
+        for (int c = lane; c < n; c += 64) st<16, POL>(o + (int64_t)c * 16, (uint32_t)c);
+    } else {
+        for (int k = 0; k < ke; k++)
+            for (int c = lane; c < cpe; c += 64) st<16, POL>(o + (int64_t)k * env_bytes + (int64_t)c * 16, (uint32_t)c);
+    }
 }
 
 int main()
@@ -104,9 +144,63 @@ int main()
     using P0 = std::integral_constant<int, 0>;
     using P1 = std::integral_constant<int, 1>;
     using P2 = std::integral_constant<int, 2>;
-    run(I16{}, P0{}); run(I16{}, P1{}); run(I16{}, P2{});
-    run(I8{}, P0{});  run(I8{}, P1{});
-    run(I4{}, P0{});  run(I4{}, P1{});
+    if (getenv("SUB_ONLY") == nullptr) {
+        run(I16{}, P0{}); run(I16{}, P1{}); run(I16{}, P2{});
+        run(I8{}, P0{});  run(I8{}, P1{});
+        run(I4{}, P0{});  run(I4{}, P1{});
+    }
+    auto runsub = [&](auto pc) {
+        constexpr int POL = decltype(pc)::value;
+        const char *pn = POL == 0 ? "wb" : (POL == 1 ? "nt" : "sc01");
+        for (int K : {1, 2, 4, 8})
+            for (int wpb : {1, 4}) {
+                const int sub = 3872;
+                const int64_t nw = 65536 / K;
+                char nm[160];
+                snprintf(nm, sizeof nm, "W16 %-4s interleaved envs: %d x %d per wave, wpb %d", pn, K, sub, wpb);
+                timeit(nm, [&](uint8_t *o) {
+                    hipLaunchKernelGGL((k_sub<16, POL>), dim3((unsigned)((nw + wpb - 1) / wpb)), dim3(64 * wpb), 0, 0, o, nw,
+                                       sub, K);
+                });
+                snprintf(nm, sizeof nm, "W16 %-4s contiguous envs:  %d x %d per wave, wpb %d", pn, K, sub, wpb);
+                timeit(nm, [&](uint8_t *o) {
+                    hipLaunchKernelGGL((k_seg<16, POL>), dim3((unsigned)((nw + wpb - 1) / wpb)), dim3(64 * wpb), 0, 0, o, in,
+                                       bytes, sub * K, 0);
+                });
+            }
+    };
+    if (getenv("ENV_PATTERN")) {
+        for (int pol = 0; pol < 2; pol++)
+            for (int K : {1, 2, 4, 8})
+                for (int region = 0; region < 2; region++) {
+                    const int64_t waves = (65536 + K - 1) / K;
+                    char nm[160];
+                    snprintf(nm, sizeof nm, "W16 %-4s %d envs per wave, %s", pol ? "nt" : "wb", K,
+                             region ? "aligned 1 KB over the region" : "env by env");
+                    timeit(nm, [&](uint8_t *o) {
+                        if (pol && region) hipLaunchKernelGGL((k_envs<1, true>), dim3((unsigned)waves), dim3(64), 0, 0, o, 65536, 3872, K);
+                        else if (pol) hipLaunchKernelGGL((k_envs<1, false>), dim3((unsigned)waves), dim3(64), 0, 0, o, 65536, 3872, K);
+                        else if (region) hipLaunchKernelGGL((k_envs<0, true>), dim3((unsigned)waves), dim3(64), 0, 0, o, 65536, 3872, K);
+                        else hipLaunchKernelGGL((k_envs<0, false>), dim3((unsigned)waves), dim3(64), 0, 0, o, 65536, 3872, K);
+                    });
+                }
+        return 0;
+    }
+    if (getenv("SEG_SWEEP")) {
+        for (int pol = 0; pol < 2; pol++)
+            for (int seg : {1024, 2048, 3072, 3872, 3968, 4096, 4224, 6144, 7744, 8192, 12288, 15488, 16384, 32768})
+                for (int wpb : {1, 4}) {
+                    const int64_t waves = (bytes + seg - 1) / seg;
+                    char nm[160];
+                    snprintf(nm, sizeof nm, "W16 %-4s seg %6d wpb %d", pol ? "nt" : "wb", seg, wpb);
+                    timeit(nm, [&](uint8_t *o) {
+                        if (pol) hipLaunchKernelGGL((k_seg<16, 1>), dim3((unsigned)((waves + wpb - 1) / wpb)), dim3(64 * wpb), 0, 0, o, in, bytes, seg, 0);
+                        else hipLaunchKernelGGL((k_seg<16, 0>), dim3((unsigned)((waves + wpb - 1) / wpb)), dim3(64 * wpb), 0, 0, o, in, bytes, seg, 0);
+                    });
+                }
+        return 0;
+    }
+    runsub(P0{}); runsub(P1{}); runsub(P2{});
     (void)hipFree(buf);
     (void)hipFree(in);
     return 0;

@@ -147,17 +147,39 @@ BATCH_CASES = {
     'big_44_s4_global_links': (dict(height=44, width=44, snake_length=3, vision_range=4, spawn_ahead=4), 4, 16, 200),
     # 100x100: k_logic's eight frames per wave take 80 KB of LDS, one wave per workgroup
     'big_100_l2': (dict(height=100, width=100, snake_length=2, vision_range=3), 4, 16, 120),
+    # the fused one-launch step (k_step: one frame, <= 4 snakes, table encode,
+    # in-step spawn-ahead -- spawn_background=-1 keeps these small batches off
+    # the background kernel): vision crop, full map, coop, human observer,
+    # truncation, two snakes, eight lanes per env (N <= 8192)
+    'fused_vr5_s4': (dict(height=20, width=20, snake_length=3, vision_range=5, spawn_background=-1), 4, 128, 300),
+    'fused_full20_s4': (dict(height=20, width=20, snake_length=3, spawn_background=-1), 4, 96, 300),
+    'fused_coop_vr5_s4': (dict(height=20, width=20, vision_range=5, coop=True, spawn_background=-1), 4, 96, 300),
+    'fused_human_12_vr3': (dict(height=12, width=12, vision_range=3, observer='human', spawn_background=-1), 4, 64, 300),
+    'fused_trunc_12_s2': (dict(height=12, width=12, max_episode_steps=7, spawn_background=-1), 2, 64, 100),
+    'fused_s2_vr4': (dict(height=12, width=12, vision_range=4, num_fruits=6, spawn_background=-1), 2, 64, 300),
 }
 
 
+@pytest.fixture
+def fused_on():
+    """The fused one-launch step (k_step) switched on for the test
+    (snake_debug_set "fused"; off by default until it wins)."""
+    from marlenv import _native
+    _native.debug_set('fused', 1)
+    yield
+    _native.debug_set('fused', 0)
+
+
 @pytest.mark.parametrize('case', sorted(BATCH_CASES))
-def test_batch_matches_oracle(oracle, case):
+def test_batch_matches_oracle(oracle, case, request):
     from marlenv import SnakeVecEnv
+    if case.startswith('fused_'):
+        request.getfixturevalue('fused_on')
     kw, S, N, T = BATCH_CASES[case]
     seed = 1000 + 17 * len(case)
     v = SnakeVecEnv(N, num_snakes=S, seed=seed, **kw)
     obs0 = _np(v.reset())
-    okw = {k: x for k, x in kw.items() if k != 'spawn_ahead'}   # a GPU scheduling knob only
+    okw = {k: x for k, x in kw.items() if k not in ('spawn_ahead', 'spawn_background')}   # GPU scheduling knobs only
     refs, robs = oracle_batch(oracle, N, seed, S, **okw)
     np.testing.assert_array_equal(obs0, robs)
     rs = np.random.RandomState(seed)
@@ -167,6 +189,31 @@ def test_batch_matches_oracle(oracle, case):
         obs, rew, done, info = v.step(torch.from_numpy(a))
         compare_step(refs, range(N), a, _np(obs), _np(rew), _np(done), _np(info),
                      grids=_np(v.grids()), where=f'{case} step {t}')
+
+
+@pytest.mark.parametrize('N,kw,fused', [
+    (256, dict(height=20, width=20, vision_range=5, spawn_background=-1), True),
+    (256, dict(height=20, width=20, spawn_background=-1), True),
+    (256, dict(height=20, width=20, vision_range=5), False),            # (small batch: background spawn kernel)
+    (128, dict(height=40, width=40, vision_range=5, frame_stack=4), False),
+])
+def test_fused_step_is_used(N, kw, fused, fused_on):
+    """The one-launch step (k_step) runs exactly where snake_plan enables it."""
+    from marlenv import SnakeVecEnv, _native
+    v = SnakeVecEnv(N, num_snakes=4 if kw['height'] == 20 else 8, seed=1, **kw)
+    v.reset()
+    S = v.num_snakes
+    for k in ('k_step', 'k_logic', 'k_post'):
+        _native.timing_read(k)
+    _native.timing_enable(True)
+    try:
+        v.step(torch.zeros((N, S), dtype=torch.int8, device='cuda'))
+    finally:
+        _native.timing_enable(False)
+    n_step, n_logic = _native.timing_read('k_step')[1], _native.timing_read('k_logic')[1]
+    assert (n_step, n_logic) == ((1, 0) if fused else (0, 1))
+    assert _native.timing_read('fused_timeout')[1] == 0
+    v.close()
 
 
 def test_coop_any_done(oracle):
@@ -662,6 +709,40 @@ def test_every_step_invalid_action_keeps_obs(oracle, kw, S):
             assert rr.tobytes() == rew[i].tobytes()
             last[i] = r.reset()
             np.testing.assert_array_equal(obs[i], last[i], err_msg=f'step {t} env {i}')
+
+
+@pytest.mark.parametrize('kw,S', [(dict(height=20, width=20, vision_range=5), 4),
+                                  (dict(height=12, width=12), 3)])
+def test_fused_invalid_action_keeps_obs(oracle, kw, S, fused_on):
+    """The fused step (k_step) with invalid actions in some envs: a rejected env
+    is left unchanged and its observation is that of its unchanged state (the
+    logic wave hands the encodes its old slot and heads); every other env steps
+    (and auto-resets) exactly like the oracle."""
+    from marlenv import SnakeVecEnv
+    N = 64
+    v = SnakeVecEnv(N, num_snakes=S, seed=17, spawn_background=-1, **kw)
+    refs, o0 = oracle_batch(oracle, N, 17, S, **kw)
+    assert (_np(v.reset()) == o0).all()
+    last = o0.copy()
+    rs = np.random.RandomState(4)
+    for t in range(80):
+        a = rs.randint(0, 3, size=(N, S))
+        bad = rs.rand(N) < 0.2
+        a[bad, 0] = 9
+        obs, rew, done, info = v.step(torch.from_numpy(a))
+        obs, rew, done, err = _np(obs), _np(rew), _np(done), _np(info['error'])
+        for i, r in enumerate(refs):
+            try:   # (the reference raises KeyError only for an ALIVE snake's invalid action)
+                ro, rr, rd, _ = r.step(a[i])
+            except KeyError:
+                assert bad[i] and err[i] == 1 and not rew[i].any() and not done[i].any(), (t, i)
+                np.testing.assert_array_equal(obs[i], last[i], err_msg=f'step {t} env {i}')
+                continue
+            if all(rd):
+                ro = r.reset()
+            assert err[i] == 0 and rr.tobytes() == rew[i].tobytes(), (t, i)
+            np.testing.assert_array_equal(obs[i], ro, err_msg=f'step {t} env {i}')
+            last[i] = ro
 
 
 def test_full_size_cfg2_every_env(oracle):
