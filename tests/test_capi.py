@@ -54,7 +54,9 @@ def test_plan_sizes(native):
     assert lay.spawn == 65536 * 672 * 4                        # spawn-ahead records
     assert lay.stats == 65536 * 4 * 16                         # snake_epi_stat: one 16-B record per snake
     # two sets (step parity) of three queues + counters (one per 128-B line)
-    assert lay.resetq == 2 * (3 * 64 * (4096 // 64) * 16 + 227 * 32) * 4
+    # two queue sets, then the fused step's counts, flags and hand-off records
+    queues = 2 * (3 * 64 * (4096 // 64) * 16 + 227 * 32)
+    assert lay.resetq == (queues + 64 * 32 + 2 * 65536 // 4 + 4 * 65536) * 4
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
     assert lay.obs_c == 32 and lay.obs == 8192 * 8 * 11 * 11 * 32
