@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SNAKE_ABI_VERSION 16
+#define SNAKE_ABI_VERSION 17
 
 #define SNAKE_OK           0
 #define SNAKE_E_CONFIG    -1   /* invalid snake_cfg (message says which field) */
@@ -57,7 +57,7 @@ typedef struct {
                                    8192 spawn poses, every env under coop), -1 = off, k >= 1 =
                                    envs with at most k live snakes. Never changes results. */
     int32_t spawn_background;   /* 1 = the spawn-ahead attempts run in a background kernel on a
-                                   stream of the library's (one per queue set) that outlives snake_step (see
+                                   stream of the library's (two per state) that outlives snake_step (see
                                    snake_sync, snake_release), 0 = automatic (on for boards of
                                    more than 8192 spawn poses, e.g. 40x40, and for batches of
                                    at most 8192 envs and 64 MiB of observations per step),
@@ -77,9 +77,9 @@ typedef struct {
                                                          624 + j = word j of the next key),
                                                          spawn-ahead status word (bits 0-1: 0 none,
                                                          1 partial, 2 ready, 3 being drawn by a background
-                                                         job; bit 2: which of the env's two
-                                                         records holds it (background spawn-ahead); bits
-                                                         3-31: the record's generation),
+                                                         job; bits 2-3: which of the env's four
+                                                         records holds it (background spawn-ahead, one per
+                                                         queue set); bits 4-31: the record's generation),
                                                          spawn failure (1: the last reset gave up, below);
                                                          words 6-7 unused */
     int64_t ctr;        /* uint16 [N][fs][S]             crop centre (r<<8|c) of each grid ring slot */
@@ -92,10 +92,12 @@ typedef struct {
                                                          four-wave lean encodes (k_post_lean) */
     int64_t spawn;      /* uint32 [N][672]               spawn-ahead record: MT key, MT pos and the
                                                          S*L spawn cells (u16) of the env's next reset
-                                                         ([2][N][672] with background spawn-ahead) */
-    int64_t resetq;     /* int32  2 x ([3][64][cap] + [227*32]) sharded auto-reset and spawn-ahead
+                                                         ([4][N][672] with background spawn-ahead) */
+    int64_t resetq;     /* int32  4 x ([3][64][cap] + [227*32]) sharded auto-reset and spawn-ahead
                                                          queues + the step's counters, one per 128-B
-                                                         line; two sets, by step parity (zero-initialised) */
+                                                         line; four sets, by step count mod 4; then the
+                                                         fused step's flags and hand-off records
+                                                         (zero-initialised) */
     int64_t obs;        /* uint8  [N][S][h][w][8*fs]     NHWC observations */
     int64_t rew;        /* double [N][S] */
     int64_t done;       /* uint8  [N][S] */

@@ -348,6 +348,9 @@ int64_t fused_base(int64_t N)
 }
 int64_t fused_words(int64_t N)
 {
+#ifdef SNAKE_NO_FUSED_AREA
+    return 0 * N;
+#endif
     return kQShards * kQSpread + 2 * round_up((N + 3) / 4, 4) + 4 * N;
 }
 
@@ -385,8 +388,8 @@ int layout_of(const snake_cfg *c, int64_t N, snake_layout *o)
     const bool lean_workers = c->autoreset == 1 && lean_geom(c).lean;
     o->jscratch = (round_up(2 * (o->n_cand + kWave), 16) <= kJarrLdsMax && !lean_workers)
                       ? 0 : std::min<int64_t>(N, kResetSlots) * link;
-    // (background spawn-ahead: two records per env, see k_spawn)
-    o->spawn = (bg_of(c, o->n_cand, N) ? 2 : 1) * N * kSpawnStride * 4;
+    // (background spawn-ahead: one record per queue set and env, see k_spawn)
+    o->spawn = (bg_of(c, o->n_cand, N) ? kQSets : 1) * N * kSpawnStride * 4;
     {   // auto-reset and spawn-ahead queues: kQShards shards each (k_logic block %
         // kQShards) with room for every env of its blocks, + the step's counters
         // (kQCount, each in its own line); sized for any k_logic lane grouping
@@ -547,9 +550,12 @@ int build_kcfg(const snake_cfg *c, int64_t N, int64_t n_cand, KCfg *k)
     // 512 0.0827-0.0832, 1 024 0.0822, 2 048 0.0823)
     k->spawn_slots = (int)std::min<int64_t>(N, bg_small ? 512 : kResetSlots);
 #ifndef SNAKE_BG_TRIES_SMALL
-#define SNAKE_BG_TRIES_SMALL 1
+#define SNAKE_BG_TRIES_SMALL 2
 #endif
-    // k_spawn: attempts per job (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
+    // k_spawn: attempts per job. Two on small background boards since the four
+    // queue sets (round 6, same box, ms per step: cfg2 0.0397 -> 0.0380, cfg3s8
+    // 0.0414 -> 0.0401; four tries slower, profiles/r06_ab_qsets.txt); one on
+    // 40x40 (4 measured 0.30 ms at cfg5: the kernel then gates k_logic)
     k->bg_tries = bg_small ? SNAKE_BG_TRIES_SMALL : 1;
     k->spawn_tries = 1;   // attempts per in-step spawn-ahead job (2 measured cfg3 0.0875 -> 0.103 ms: a retry doubles the chain)
     k->lds_obs_bytes = off;

@@ -40,17 +40,26 @@ constexpr int kQSpDone = kQSpClaim + kClaimShards;    // k_spawn: claim shards d
 constexpr int kQSpGen = kQSpDone + 1;
 constexpr int kQCount = kQSpGen + 1;                  // counters
 constexpr int kQCounters = kQCount * kQSpread;        // words
-// The queues and counters exist twice (the step's parity, KCfg.qpar): with the
-// background spawn kernel a step's spawn-ahead queues are still being read while
-// the next step's k_logic fills the other set.
-constexpr int kQSets = 2;
+// The queues and counters exist kQSets times (the step count mod kQSets,
+// KCfg.qpar): with the background spawn kernel a step's spawn-ahead queues are
+// still being read while the next steps' k_logic fill the other sets; a set is
+// refilled only once its previous spawn kernel has finished (kQSpGen). Four
+// sets (round 6; two until then): a spawn kernel may run for three steps before
+// it holds up the queueing, so its jobs can afford more than one attempt.
+#ifndef SNAKE_QSETS
+#define SNAKE_QSETS 4
+#endif
+constexpr int kQSets = SNAKE_QSETS;   // (2 or 4: the status word's two buffer bits)
+static_assert(kQSets == 2 || kQSets == 4, "two or four queue sets");
 constexpr int kQGenBits = 6;        // spawn queue entry (background mode): env | generation << 26
 
 // env record words (6, 7 unused)
 enum { ENV_ALIVE = 0, ENV_EPLEN = 1, ENV_CUR = 2, ENV_MTPOS = 3, ENV_SPAWN = 4, ENV_FAIL = 5 };
-// spawn-ahead status word (env word ENV_SPAWN): bits 0-1 the status, bit 2 the
-// record buffer holding the record (background spawn-ahead keeps two per env),
-// bits 3-31 the record's generation (bumped by every MT draw that voids it)
+// spawn-ahead status word (env word ENV_SPAWN): bits 0-1 the status, bits 2-3 the
+// record buffer holding the record (background spawn-ahead keeps one per queue
+// set and env), bits 4-31 the record's generation (bumped by every MT draw that
+// voids it)
+constexpr int kSpawnBufShift = 2, kSpawnGenShift = 4;
 // DRAWING (background spawn-ahead only): a k_spawn job is drawing the record
 // (from the env's own MT state or the partial record the buffer bit points at)
 enum { SPAWN_NONE = 0, SPAWN_PARTIAL = 1, SPAWN_READY = 2, SPAWN_DRAWING = 3 };

@@ -351,6 +351,12 @@ __device__ __forceinline__ void obs_store_edge(T *p, const T &v, int x, int lf, 
     else obs_store(p, v);
 }
 
+// k_logic with one frame writes back only the 16-byte chunks of the frame the
+// step changed (0: the whole frame, as before round 6)
+#ifndef SNAKE_LOGIC_DIRTY
+#define SNAKE_LOGIC_DIRTY 1
+#endif
+
 constexpr int kRespawnT = 4;   // raws per lane prefetched by the fast fruit respawn
 
 __device__ __forceinline__ uint32_t gen_mask(uint32_t m)
@@ -1096,7 +1102,7 @@ __device__ bool spawn_attempt(const KCfg &c, const snake_state &st, WaveMT &mt, 
 // Spawn-ahead status word (env word ENV_SPAWN): bits 0-1 the status, bit 2 the
 // record buffer holding the record (background spawn-ahead keeps two per env,
 // k_spawn), bits 3-31 the generation (bumped by every draw that voids it).
-constexpr uint32_t kGenOne = 8;
+constexpr uint32_t kGenOne = 1u << kSpawnGenShift;
 __device__ __forceinline__ uint32_t *spawn_rec(const KCfg &c, const snake_state &st, int64_t e, int b)
 {
     return st.spawn + ((int64_t)b * c.N + e) * kSpawnStride;
@@ -1208,7 +1214,7 @@ __device__ __forceinline__ int claim_reset_mt(const KCfg &c, const snake_state &
     if ((spw & 3) == SPAWN_DRAWING) spw &= ~3;   // (still drawing: from the env's own state, as for NONE)
     cellw = 0;
     if ((spw & 3) != SPAWN_NONE) {
-        const uint32_t *rec = spawn_rec(c, st, e, (spw >> 2) & 1);
+        const uint32_t *rec = spawn_rec(c, st, e, (spw >> kSpawnBufShift) & (kQSets - 1));
         mt_load_sc1(mt, rec, (int)ld_sc1(rec + kSpawnPos), lane);
         cellw = ld_sc1(rec + kSpawnCells + (lane >> 1));
     } else {
@@ -1314,7 +1320,7 @@ __device__ __forceinline__ void reset_paint(const KCfg &c, const snake_state &st
         er.x = S; er.y = 0; er.z = c.fs - 1; er.w = mt.pos;
         *reinterpret_cast<int4 *>(st.env + (int64_t)e * kEnvRec) = er;
         // record used up (background: the claim's bumped generation, buffer 0)
-        if (c.bg) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)((((uint32_t)spw >> 3) + 1u) << 3);
+        if (c.bg) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = (int)((((uint32_t)spw >> kSpawnGenShift) + 1u) << kSpawnGenShift);
         else if (spst != SPAWN_NONE) st.env[(int64_t)e * kEnvRec + ENV_SPAWN] = spw & ~3;
         st.env[(int64_t)e * kEnvRec + ENV_FAIL] = failed ? 1 : 0;
         if (failed && o.err) o.err[e] = 2;
@@ -1661,17 +1667,25 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     // phase-1 cell is rewritten in phase 2 only by a snake entering that tail,
     // which is what the reference's index-ordered updates produce.
     LSTAMP(42);
+    // One frame (fs == 1): the slot is rewritten in place, so only the 16-byte
+    // chunks this step writes go back to it (bit q of dm = chunk q of the frame,
+    // frames of up to 64 chunks); the commit below ORs the group's masks
+    uint64_t dm = 0;
+    auto dirty = [&](int cell) { dm |= 1ull << (((unsigned)cell >> 4) & 63u); };
     const int pt = tr * W + tc;
     if (alive && !eat) {
         if (work[pt] == C_TAIL + 10 * k) work[pt] = C_EMPTY;
+        dirty(pt);
     }
     if (isn && death) {
         if (div10(work[pt]) == k) work[pt] = C_EMPTY;
+        dirty(pt);
     }
     wave_sync();
     int nhr = hr, nhc = hc, ntr = tr, ntc = tc;
     if (alive) {
         work[hr * W + hc] = (uint8_t)(C_BODY + 10 * k);
+        dirty(hr * W + hc);
         nhr = hr + dir_dr(dir);
         nhc = hc + dir_dc(dir);
         rh = (rh - 1) & (cap - 1);                                   // directions.appendleft
@@ -1717,6 +1731,8 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
         }
         work[nhr * W + nhc] = (uint8_t)(C_HEAD + 10 * k);
         work[ntr * W + ntc] = (uint8_t)(C_TAIL + 10 * k);
+        dirty(nhr * W + nhc);
+        dirty(ntr * W + ntc);
     }
     wave_sync();
     // draw(grid, coords, EMPTY) of each dying snake's head and body (the tail was
@@ -1728,6 +1744,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
         const uint8_t *rk = ring;
         int br = hr, bc = hc;
         work[br * W + bc] = C_EMPTY;
+        dirty(br * W + bc);
         const int n = rl - 1;
         for (int m0 = 0; m0 < n; m0 += 16) {
             int d[16];
@@ -1753,6 +1770,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
                     br -= dir_dr(d[t]);
                     bc -= dir_dc(d[t]);
                     work[br * W + bc] = C_EMPTY;
+                    dirty(br * W + bc);
                 }
             }
         }
@@ -1846,7 +1864,10 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
             }
         }
         wave_sync();
-        if (fast && k < fruit_taken) work[cellbuf[k]] = C_FRUIT;
+        if (fast && k < fruit_taken) {
+            work[cellbuf[k]] = C_FRUIT;
+            dirty(cellbuf[k]);
+        }
         if (fast && draws) mtpos_new = mtpos + used;
         fast_done = fast;
         wave_sync();
@@ -1873,7 +1894,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
         } else {
             mt_store(mt, st.mt + ee * kMtN, lane);
         }
-        if (g == gg) { mtpos_new = mt.pos; mt_slow = true; }
+        if (g == gg) { mtpos_new = mt.pos; mt_slow = true; dm = ~0ull; }
     }
     // a draw from the MT state voids the env's spawn-ahead record
     const bool drew = mt_slow || mtpos_new != mtpos;
@@ -1882,7 +1903,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     // first, is overwritten here; so with bg every draw writes the word)
     const bool spw_wr = drew && (BG || spst != SPAWN_NONE);
     if (c.diag && drew && spst == SPAWN_READY && k == 0) DIAG_ADD(g_spawn_void);
-    const uint32_t spw1 = drew ? (((uint32_t)er2.x >> 3) + 1u) << 3 : (uint32_t)er2.x;
+    const uint32_t spw1 = drew ? (((uint32_t)er2.x >> kSpawnGenShift) + 1u) << kSpawnGenShift : (uint32_t)er2.x;
 
     LSTAMP(45);
     // episode statistics (:385-389), truncation (:391-394), rank/info (:396-412)
@@ -1911,7 +1932,7 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
         }
     }
     // and the spawn-ahead jobs (background: with the generation they were queued at)
-    const int pent = BG ? (int)((uint32_t)e | ((spw1 >> 3) << (32 - kQGenBits))) : e;
+    const int pent = BG ? (int)((uint32_t)e | ((spw1 >> kSpawnGenShift) << (32 - kQGenBits))) : e;
     if (pm) {
         const int base = bcast(pbase, 0);
         if ((pm >> lane) & 1ull) {
@@ -1952,16 +1973,28 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
     }
 
     LSTAMP(46);
-    // commit the new frames into their ring slots; records; crop centres
+    // commit the new frames into their ring slots (one frame: the chunks the
+    // step wrote, in place); records; crop centres
     {
         uint4 *dst = reinterpret_cast<uint4 *>(st.grid);
         const uint4 *s4 = reinterpret_cast<const uint4 *>(lds);
+        const bool inplace = SNAKE_LOGIC_DIRTY && fs == 1 && n16 <= 64;
+        uint32_t dlo = ~0u, dhi = ~0u;
+        if (inplace) {
+            dlo = dhi = 0u;
+            unroll<G>([&](auto J) {
+                dlo |= (uint32_t)gsel<G, J>((int)(uint32_t)dm);
+                dhi |= (uint32_t)gsel<G, J>((int)(uint32_t)(dm >> 32));
+            });
+        }
         for (int q0 = 0; q0 < E * n16; q0 += kWave) {
             const int q = q0 + lane, gg = min(fdiv((uint32_t)q, c.mag_n16, n16), E - 1);
             const int off = q - gg * n16;
             const int ng = __shfl(ncur, gg * G);
             const int bg = __shfl((int)(bad || (FU && ep_end)), gg * G);
-            if (q < E * n16 && e0 + gg < c.N && !bg) {
+            const uint32_t ml = (uint32_t)__shfl((int)dlo, gg * G), mh = (uint32_t)__shfl((int)dhi, gg * G);
+            const bool wrote = ((off < 32 ? ml >> off : mh >> (off & 31)) & 1u) != 0u;
+            if (q < E * n16 && e0 + gg < c.N && !bg && wrote) {
                 uint4 *d = dst + ((int64_t)(e0 + gg) * c.ring_bytes + (int64_t)ng * stride) / 16 + off;
                 if constexpr (FU) st_sc1_128(d, s4[q]);   // (the encodes read it in this launch)
                 else *d = s4[q];
@@ -2052,7 +2085,8 @@ __device__ void store_spawn_record(const KCfg &c, const snake_state &st, int e, 
     const uint32_t cw = ((uint32_t)cell & 0xffffu) | ((uint32_t)nxt << 16);
     const bool cst = ok && (lane & 1) == 0 && lane < c.S * c.L;
     uint32_t *wp = reinterpret_cast<uint32_t *>(st.env + (int64_t)e * kEnvRec + ENV_SPAWN);
-    const uint32_t w1 = (spw & ~7u) | ((uint32_t)nb << 2) | (ok ? SPAWN_READY : SPAWN_PARTIAL);
+    const uint32_t w1 = (spw & ~((1u << kSpawnGenShift) - 1u)) | ((uint32_t)nb << kSpawnBufShift) |
+                        (ok ? SPAWN_READY : SPAWN_PARTIAL);
     if constexpr (BG) {
 #pragma unroll
         for (int t = 0; t < 10; t++)
@@ -2116,7 +2150,7 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
     if (lane == 0) v = (int)atomicAdd(wp, 0u);   // (the memory-side value)
     uint32_t spw = (uint32_t)__shfl(v, 0);
     // (READY: nothing to do; DRAWING: another job -- an earlier step's -- has it)
-    if (((spw >> 3) & ((1u << kQGenBits) - 1u)) != qgen || (spw & 3u) >= SPAWN_READY) return;
+    if (((spw >> kSpawnGenShift) & ((1u << kQGenBits) - 1u)) != qgen || (spw & 3u) >= SPAWN_READY) return;
     const uint32_t st0 = spw & 3u;
     {
         // mark the record as being drawn: claim_reset_mt waits for it, and a job
@@ -2134,7 +2168,7 @@ __device__ void do_spawn_bg(const KCfg &c, const snake_state &st, int e, uint32_
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned)c.spawn_delay) __builtin_amdgcn_s_sleep(32);
     }
-    const int buf = (spw >> 2) & 1;
+    const int buf = (spw >> kSpawnBufShift) & (kQSets - 1);
     WaveMT mt;
     if (st0 != SPAWN_NONE) {
         const uint32_t *rec = spawn_rec(c, st, e, buf);
@@ -2603,9 +2637,15 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
                 for (int t = 0; t < CP; t++)
                     r[t] = lookup(reinterpret_cast<const uint2 *>(desc)[min(q0 + t * T + lane, chunks - 1)]);
 #pragma unroll
-                for (int t = 0; t < CP; t++)
-                    if (q0 + t * T + lane < chunks)
-                        obs_store_edge(out + q0 + t * T + lane, r[t], 16 * (q0 + t * T + lane), lf, hf);
+                for (int t = 0; t < CP; t++) {
+                    if (q0 + t * T + lane < chunks) {
+                        // (four-wave encodes, cfg5: no edge test -- its branch in
+                        // this loop cost k_post_lean 57 -> 75 us, round 6; the envs
+                        // there fill whole lines anyway)
+                        if constexpr (T == kWave) obs_store_edge(out + q0 + t * T + lane, r[t], 16 * (q0 + t * T + lane), lf, hf);
+                        else obs_store(out + q0 + t * T + lane, r[t]);
+                    }
+                }
             }
             }
         }
@@ -3090,13 +3130,18 @@ constexpr unsigned kJoinFlags = hipEventDisableTiming | hipEventDisableSystemFen
 // with one stream they queued behind each other (a 40x40 job takes about a
 // step) and k_logic found its set's previous kernel unfinished in ~21 % of
 // cfg5's steps, queued nothing, and the next step's resets drew inline.
+constexpr int kBgStreams = 2;
 struct BgCtx {
-    hipStream_t x[2] = {nullptr, nullptr};
+    // (two streams for the four queue sets, set p on stream p % 2: every
+    // stream takes one of the process's hardware queues -- GPU_MAX_HW_QUEUES,
+    // 4 by default -- and with four background streams the caller's stream
+    // shared one with a spawn kernel: cfg5 0.0811 -> 0.0980 ms, round 6)
+    hipStream_t x[kBgStreams] = {};
     hipEvent_t fork = nullptr;
-    hipEvent_t done[2] = {nullptr, nullptr};
+    hipEvent_t done[kQSets] = {};
     uint64_t steps = 0;
-    bool pending[2] = {false, false};
-    uint32_t launched[2] = {0, 0};   // k_spawn launches per queue set (KCfg.spawn_gate)
+    bool pending[kQSets] = {};
+    uint32_t launched[kQSets] = {};   // k_spawn launches per queue set (KCfg.spawn_gate)
 };
 static std::mutex g_bgmu;
 static std::map<const void *, BgCtx> g_bg;
@@ -3108,7 +3153,8 @@ static void destroy_bg(BgCtx &c)
 {
     for (hipStream_t x : c.x)
         if (x) (void)hipStreamSynchronize(x);   // (its last k_spawn)
-    for (hipEvent_t ev : {c.fork, c.done[0], c.done[1]})
+    if (c.fork) (void)hipEventDestroy(c.fork);
+    for (hipEvent_t ev : c.done)
         if (ev) (void)hipEventDestroy(ev);
     for (hipStream_t x : c.x)
         if (x) (void)hipStreamDestroy(x);
@@ -3122,13 +3168,14 @@ static BgCtx *bg_ctx(const snake_state &st, bool create)
     if (it != g_bg.end()) return &it->second;
     if (!create) return nullptr;
     BgCtx c;
-    if (hipStreamCreateWithFlags(&c.x[0], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c.x[1], hipStreamNonBlocking) != hipSuccess ||
-        // (the fork event rides on k_logic's dispatch as its stop event, like
-        // the timing events: a timing-capable event without the system fence)
-        hipEventCreateWithFlags(&c.fork, hipEventDisableSystemFence) != hipSuccess ||
-        hipEventCreateWithFlags(&c.done[0], kJoinFlags) != hipSuccess ||
-        hipEventCreateWithFlags(&c.done[1], kJoinFlags) != hipSuccess) {
+    bool ok = true;
+    for (int p = 0; p < kBgStreams && ok; p++)
+        ok = hipStreamCreateWithFlags(&c.x[p], hipStreamNonBlocking) == hipSuccess;
+    for (int p = 0; p < kQSets && ok; p++)
+        ok = hipEventCreateWithFlags(&c.done[p], kJoinFlags) == hipSuccess;
+    // (the fork event rides on k_logic's dispatch as its stop event, like the
+    // timing events: a timing-capable event without the system fence)
+    if (!ok || hipEventCreateWithFlags(&c.fork, hipEventDisableSystemFence) != hipSuccess) {
         destroy_bg(c);
         set_error("background stream / event creation failed");
         return nullptr;
@@ -3141,7 +3188,7 @@ int wait_background(const snake_state &st, void *stream)
 {
     BgCtx *b = bg_ctx(st, false);
     if (!b) return SNAKE_OK;
-    for (int p = 0; p < 2; p++)
+    for (int p = 0; p < kQSets; p++)
         if (b->pending[p] && hipStreamWaitEvent((hipStream_t)stream, b->done[p], 0) != hipSuccess) {
             set_error("waiting for the background spawn kernel failed");
             return SNAKE_E_LAUNCH;
@@ -3283,7 +3330,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
                   // it so far have finished (kQSpGen), the stream never waits
                   // (the wait cost cfg5 0.1026 -> 0.1136 ms per step)
         if (!(bgc = bg_ctx(st, true))) return SNAKE_E_LAUNCH;
-        k.qpar = (int)(bgc->steps & 1);
+        k.qpar = (int)(bgc->steps % kQSets);
         k.spawn_gate = bgc->launched[k.qpar];
     }
     if (k.fused && g_fused) {   // the whole step as one launch (k_step)
@@ -3396,7 +3443,7 @@ int launch_step(const KCfg &k0, const snake_state &st, const int8_t *actions, co
         // this step's spawn kernel on the background stream once k_logic has
         // passed (its dispatch's stop event, above); not joined (k_logic two
         // steps later only queues into the set once it has finished)
-        hipStream_t bx = bgc->x[k.qpar];
+        hipStream_t bx = bgc->x[k.qpar % kBgStreams];
         if (hipStreamWaitEvent(bx, fork_ev, 0) != hipSuccess) {
             set_error("fork to the background stream failed");
             return fail(SNAKE_E_LAUNCH);

@@ -28,6 +28,7 @@ from marlenv import SnakeVecEnv, _native  # noqa: E402
 CFGS = {'cfg3': (65536, 4, dict(height=20, width=20, vision_range=5)),
         'cfg4': (32768, 4, dict(height=20, width=20, vision_range=5)),
         'cfg2': (4096, 4, dict(height=20, width=20)),
+        'cfg3s8': (8192, 4, dict(height=20, width=20, vision_range=5)),
         'cfg5': (8192, 8, dict(height=40, width=40, vision_range=5, frame_stack=4))}
 KWT, KPT, KIT = 8192, 40960, 16384
 TYPES = ('reset_ready', 'reset_partial', 'reset_none', 'job_q1', 'job_q2')
@@ -56,7 +57,8 @@ def main():
     acts = torch.randint(0, 3, (a.skip + a.steps, N, S), generator=g, device='cuda', dtype=torch.int8)
     buf = np.zeros(64 + 2 * KWT + 2 * KPT, np.uint64)
     items = np.zeros(4 * KIT, np.uint64)
-    G = min(N, 2048) // (4 if a.cfg == 'cfg5' else 1)   # worker blocks (k_post_lean: four workers each)
+    G = v._kcfg_reset_slots() if hasattr(v, '_kcfg_reset_slots') else min(N, 512 if N <= 8192 else 2048)
+    G = G // (4 if a.cfg == 'cfg5' else 1)   # worker blocks (k_post_lean: four workers each)
     spans, enc_ends, crit, encs, gaps, lspan = [], [], Counter(), [], [], []
     per = {t: dict(n=[], dur=[], end=[]) for t in range(5)}
     chains = Counter()

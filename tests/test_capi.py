@@ -55,7 +55,7 @@ def test_plan_sizes(native):
     assert lay.stats == 65536 * 4 * 16                         # snake_epi_stat: one 16-B record per snake
     # two sets (step parity) of three queues + counters (one per 128-B line)
     # two queue sets, then the fused step's counts, flags and hand-off records
-    queues = 2 * (3 * 64 * (4096 // 64) * 16 + 227 * 32)
+    queues = 4 * (3 * 64 * (4096 // 64) * 16 + 227 * 32)   # (four queue sets)
     assert lay.resetq == (queues + 64 * 32 + 2 * 65536 // 4 + 4 * 65536) * 4
     c = cfg(native, height=40, width=40, num_snakes=8, vision_range=5, frame_stack=4)
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay)) == 0
@@ -64,7 +64,7 @@ def test_plan_sizes(native):
     # background spawn-ahead the one-launch workers (k_post_lean) keep a global
     # link table per worker for resets without a ready record
     assert lay.n_cand == 16424 and lay.jscratch == 2048 * (16424 + 64) * 4
-    assert lay.spawn == 2 * 8192 * 672 * 4                        # background spawn-ahead: two records per env
+    assert lay.spawn == 4 * 8192 * 672 * 4                        # background spawn-ahead: a record per queue set and env
     c = cfg(native, height=44, width=44, num_snakes=4)
     lay2 = native.SnakeLayout()
     assert native.lib().snake_plan(ctypes.byref(c), 8192, ctypes.byref(lay2)) == 0
@@ -93,11 +93,11 @@ def test_plan_sizes(native):
 def test_plan_background_automatic(native, kw, N, bg):
     """spawn_background = 0 (automatic) turns the background spawn kernel on for
     batches of at most 8 192 envs and 64 MiB of observations per step (round 5):
-    the layout then holds two spawn-ahead records per env."""
+    the layout then holds a spawn-ahead record per queue set (four) and env."""
     c = cfg(native, num_snakes=4, **kw)
     lay = native.SnakeLayout()
     assert native.lib().snake_plan(ctypes.byref(c), N, ctypes.byref(lay)) == 0
-    assert lay.spawn == (2 if bg else 1) * N * 672 * 4, (kw, N)
+    assert lay.spawn == (4 if bg else 1) * N * 672 * 4, (kw, N)
 
 
 @pytest.mark.parametrize('H,W,L,N', [(50, 50, 3, 16384), (72, 72, 3, 4096), (100, 100, 2, 65536)])

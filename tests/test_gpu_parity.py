@@ -315,8 +315,8 @@ def test_full_size_sampled_parity(oracle, case):
         assert int(heads[~alive].sum()) == 0
         assert not bool(info['error'].any())
     assert n_ep > 0.005 * N * T / 60
-    if case == 'cfg3s8_8192':   # (two spawn record buffers per env: the background kernel's default here)
-        assert v.layout.spawn == 2 * N * 672 * 4
+    if case == 'cfg3s8_8192':   # (a spawn record buffer per queue set: the background kernel's default here)
+        assert v.layout.spawn == 4 * N * 672 * 4
     v.close()
 
 
