@@ -326,30 +326,11 @@ __device__ __forceinline__ void obs_store(T *p, const T &v)
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
-// The 128-byte lines an env's observation shares with its neighbours (an env of
-// 3 872 bytes, cfg3/cfg4, starts 32 bytes into a line in three of four envs):
-// byte offsets [0, lf) and [hf, bytes) of the env's observation at obs_env.
-// Those chunks are stored write-back (obs_store_edge), so the L2 merges the two
-// envs' parts of the line; as non-temporal stores each part went to memory on
-// its own. Round 6, scripts/microbench/storebw2.hip ENV_PATTERN (254 MB, four
-// 3 872-byte envs per wave, env by env): non-temporal 4.49 TB/s, write-back
-// 5.33, non-temporal with aligned 1 KB instructions 5.23.
-#ifndef SNAKE_OBS_EDGE_WB
-#define SNAKE_OBS_EDGE_WB 1
-#endif
-__device__ __forceinline__ void obs_edges(const uint8_t *obs_env, int bytes, int &lf, int &hf)
-{
-    const uint32_t lo = (uint32_t)(uintptr_t)obs_env;
-    lf = SNAKE_OBS_EDGE_WB ? (int)((0u - lo) & 127u) : 0;
-    hf = SNAKE_OBS_EDGE_WB ? bytes - (int)((lo + (uint32_t)bytes) & 127u) : bytes;
-}
-// (x: the chunk's byte offset in the env's observation)
-template <typename T>
-__device__ __forceinline__ void obs_store_edge(T *p, const T &v, int x, int lf, int hf)
-{
-    if (x < lf || x >= hf) *p = v;
-    else obs_store(p, v);
-}
+// (Round 6: storing the two 128-byte lines an env's observation shares with
+// its neighbours write-back, the rest non-temporal, measured slower in the step
+// -- the per-store edge test in the encodes' store loops cost more than the
+// merged lines saved: cfg3 0.0830 -> 0.0848 ms, driver window 0.0866 -> 0.0915,
+// cfg5 k_post_lean 57 -> 75 us; profiles/r06_ab_edge_removed.txt.)
 
 // k_logic with one frame writes back only the 16-byte chunks of the frame the
 // step changed (0: the whole frame, as before round 6)
@@ -858,8 +839,6 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
     int i = rest % c.oh;
     int k = rest / c.oh;
     const bool wide = (U & 1) == 0;
-    int lf, hf;
-    obs_edges(obs_env, 8 * U, lf, hf);
     for (int p = lane; p < pairs; p += kWave) {
         int s = slot0 + f;
         s -= (s >= fs) ? fs : 0;
@@ -877,7 +856,7 @@ __device__ void encode(const KCfg &c, const uint8_t *frames, const int *org, int
             uint4 v;
             v.x = (uint32_t)a; v.y = (uint32_t)(a >> 32);
             v.z = (uint32_t)b; v.w = (uint32_t)(b >> 32);
-            obs_store_edge(reinterpret_cast<v4u *>(obs_env + 16 * (int64_t)p), (v4u){v.x, v.y, v.z, v.w}, 16 * p, lf, hf);
+            obs_store(reinterpret_cast<v4u *>(obs_env + 16 * (int64_t)p), (v4u){v.x, v.y, v.z, v.w});
         } else {
             obs_store(reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p), a);
             if (has_b) obs_store(reinterpret_cast<unsigned long long *>(obs_env + 16 * (int64_t)p + 8), b);
@@ -2610,8 +2589,6 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
         if (!skip) {
             tsync<T>();
             v4u *out = reinterpret_cast<v4u *>(o.obs + (int64_t)e * c.units * 8);
-            int lf, hf;
-            obs_edges(o.obs + (int64_t)e * c.units * 8, c.units * 8, lf, hf);
             auto lookup = [&](uint2 dd) {   // units 2q, 2q + 1 of descriptor pair dd
                 const uint2 b0 = base[dd.x >> 16], b1 = base[dd.y >> 16];
                 const uint32_t v0 = pf[b0.x + (dd.x & 0xffffu)], v1 = pf[b1.x + (dd.y & 0xffffu)];
@@ -2625,7 +2602,7 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
                 for (int t = 0; t < 4; t++) r[t] = lookup(dr[t]);
 #pragma unroll
                 for (int t = 0; t < 4; t++)
-                    if (t * T + lane < chunks) obs_store_edge(out + t * T + lane, r[t], 16 * (t * T + lane), lf, hf);
+                    if (t * T + lane < chunks) obs_store(out + t * T + lane, r[t]);
             } else {
             // CP chunks per lane and pass, their lookup chains interleaved
             // (clamped reads; only the chunks that exist are stored); two in
@@ -2637,15 +2614,8 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
                 for (int t = 0; t < CP; t++)
                     r[t] = lookup(reinterpret_cast<const uint2 *>(desc)[min(q0 + t * T + lane, chunks - 1)]);
 #pragma unroll
-                for (int t = 0; t < CP; t++) {
-                    if (q0 + t * T + lane < chunks) {
-                        // (four-wave encodes, cfg5: no edge test -- its branch in
-                        // this loop cost k_post_lean 57 -> 75 us, round 6; the envs
-                        // there fill whole lines anyway)
-                        if constexpr (T == kWave) obs_store_edge(out + q0 + t * T + lane, r[t], 16 * (q0 + t * T + lane), lf, hf);
-                        else obs_store(out + q0 + t * T + lane, r[t]);
-                    }
-                }
+                for (int t = 0; t < CP; t++)
+                    if (q0 + t * T + lane < chunks) obs_store(out + q0 + t * T + lane, r[t]);
             }
             }
         }
