@@ -337,6 +337,9 @@ typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 #ifndef SNAKE_LOGIC_DIRTY
 #define SNAKE_LOGIC_DIRTY 1
 #endif
+#ifndef SNAKE_LOGIC_COMMIT_GROUP
+#define SNAKE_LOGIC_COMMIT_GROUP 1
+#endif
 
 constexpr int kRespawnT = 4;   // raws per lane prefetched by the fast fruit respawn
 
@@ -1966,6 +1969,24 @@ __device__ __forceinline__ void logic_body(const int blk, const LogicIn &in)
                 dhi |= (uint32_t)gsel<G, J>((int)(uint32_t)(dm >> 32));
             });
         }
+        if (SNAKE_LOGIC_COMMIT_GROUP && inplace) {
+            // each env's group commits its own dirty chunks: lane k of the group
+            // the set bits k, k + G, k + 2G, ... of the group's mask (no
+            // cross-lane moves per chunk, ~3 passes instead of E * n16 / 64)
+            // (only the frame's n16 chunks: a full-wave fruit draw marks all 64)
+            const uint64_t valid = n16 >= 64 ? ~0ull : (1ull << n16) - 1ull;
+            uint64_t m = (env_ok && !bad && !(FU && ep_end)) ? (((uint64_t)dhi << 32) | dlo) & valid : 0ull;
+            for (int j = 0; j < k; j++) m &= m - 1ull;
+            uint4 *de = dst + (int64_t)e * (c.ring_bytes / 16);   // (one frame: slot 0)
+            const uint4 *se = s4 + g * n16;
+            while (m) {
+                const int off = __ffsll((long long)m) - 1;
+                if constexpr (FU) st_sc1_128(de + off, se[off]);
+                else de[off] = se[off];
+#pragma unroll
+                for (int j = 0; j < G; j++) m &= m - 1ull;
+            }
+        } else
         for (int q0 = 0; q0 < E * n16; q0 += kWave) {
             const int q = q0 + lane, gg = min(fdiv((uint32_t)q, c.mag_n16, n16), E - 1);
             const int off = q - gg * n16;
