@@ -326,6 +326,23 @@ __device__ __forceinline__ void obs_store(T *p, const T &v)
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
+// The table encode's observation stores as raw buffer stores on the env's
+// observation (a wave-uniform descriptor: no 64-bit address per store) with an
+// explicit cache policy, SNAKE_OBS_POLICY: 0 non-temporal (as obs_store), 16
+// sc1 (write-through), 17 sc0 sc1. Round 6, same box, ms per step: write-through
+// would leave no dirty lines for the kernel-end writeback but measured slower
+// (cfg3 0.0821 -> 0.0985, cfg5 0.0812 -> 0.0982, cfg4 0.0546 -> 0.0570; cfg3s8
+// 0.0390 -> 0.0387); the buffer form itself, non-temporal, is kept: cfg4
+// 0.0556 -> 0.0549, cfg3 and the driver window equal (profiles/r06_ab_obs_policy.txt).
+#ifndef SNAKE_OBS_POLICY
+#define SNAKE_OBS_POLICY 0
+#endif
+__device__ __forceinline__ void obs_store_rs(__amdgpu_buffer_rsrc_t rs, int byte_off, v4u v)
+{
+    if constexpr (SNAKE_OBS_POLICY == 0) __builtin_amdgcn_raw_buffer_store_b128(v, rs, byte_off, 0, 2);   // (nt)
+    else __builtin_amdgcn_raw_buffer_store_b128(v, rs, byte_off, 0, SNAKE_OBS_POLICY);
+}
+
 // (Round 6: storing the two 128-byte lines an env's observation shares with
 // its neighbours write-back, the rest non-temporal, measured slower in the step
 // -- the per-store edge test in the encodes' store loops cost more than the
@@ -2609,7 +2626,7 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
         if (e + 1 < e_end) SNAKE_TBL_FETCH(e + 1);   // in flight during this env's encode
         if (!skip) {
             tsync<T>();
-            v4u *out = reinterpret_cast<v4u *>(o.obs + (int64_t)e * c.units * 8);
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(o.obs + (int64_t)e * c.units * 8, 0, c.units * 8, 0x00020000);
             auto lookup = [&](uint2 dd) {   // units 2q, 2q + 1 of descriptor pair dd
                 const uint2 b0 = base[dd.x >> 16], b1 = base[dd.y >> 16];
                 const uint32_t v0 = pf[b0.x + (dd.x & 0xffffu)], v1 = pf[b1.x + (dd.y & 0xffffu)];
@@ -2623,7 +2640,7 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
                 for (int t = 0; t < 4; t++) r[t] = lookup(dr[t]);
 #pragma unroll
                 for (int t = 0; t < 4; t++)
-                    if (t * T + lane < chunks) obs_store(out + t * T + lane, r[t]);
+                    if (t * T + lane < chunks) obs_store_rs(rs, 16 * (t * T + lane), r[t]);
             } else {
             // CP chunks per lane and pass, their lookup chains interleaved
             // (clamped reads; only the chunks that exist are stored); two in
@@ -2636,7 +2653,7 @@ __device__ void encode_tbl_block(const KCfg &c, const snake_state &st, const sna
                     r[t] = lookup(reinterpret_cast<const uint2 *>(desc)[min(q0 + t * T + lane, chunks - 1)]);
 #pragma unroll
                 for (int t = 0; t < CP; t++)
-                    if (q0 + t * T + lane < chunks) obs_store(out + q0 + t * T + lane, r[t]);
+                    if (q0 + t * T + lane < chunks) obs_store_rs(rs, 16 * (q0 + t * T + lane), r[t]);
             }
             }
         }
